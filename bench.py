@@ -1,0 +1,226 @@
+"""Benchmark: stories15M batched prefill on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+
+One step = one full forward (Llama.__call__ semantics: embedding, 6 blocks, final
+norm + lm_head on the last position) of B=256 sequences x L=256 tokens per GPU,
+start_pos 0, ids already resident in HBM, logits left in HBM; for N > 1 each rank
+owns its 256 batch rows (weak scaling, reference rows are independent:
+llama3.py:163-211) and the step ends with the single RCCL gather of every rank's
+logits to rank 0 over xGMI.  Rank 0 prints one JSON line.
+
+roofline: the dominant kernel is the fused gate|up GEMM (N = 2*FD = 1536, K = 288,
+M = 65,536 rows) — algorithmic FLOPs 2*M*K*N per launch over its mean HIP-event
+duration on the context stream, against the 157.3 TFLOP/s dense fp32 MFMA peak.
+"ffn" adds the down GEMM (the metric's "% fp32 MFMA peak on FFN GEMM").
+traffic: HBM bytes per gate|up launch from the committed rocprofv3 PMC summary
+(profiles/pmc_gateup.json, FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or null.
+cpu_baseline: the oracle (NumPy restatement of the reference, oracle/) timed on
+this host's cores on a bounded sample (B=32, L=256), rank 0 at N=1 only.
+"""
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "llama3.np_amd"))
+
+import l3hip  # noqa: E402
+import llama3  # noqa: E402
+import synth  # noqa: E402
+
+METRIC = "tokens/s stories15M batch-256 seq-256 prefill; % fp32 MFMA peak on FFN GEMM"
+PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+B_PER_GPU, SEQ = 256, 256
+
+
+class Dist:
+    """Harness-side rendezvous (gloo on the host) for the RCCL id, barriers and the
+    max-over-ranks time.  The data-path collective is RCCL inside libllama3hip."""
+
+    def __init__(self, n):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if n != self.world:
+            raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}; launch N>1 with torch.distributed.run")
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist  # host-side rendezvous only (gloo)
+
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def bcast_bytes(self, b):
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def max(self, x):
+        if self.world == 1:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def cpu_baseline():
+    """Oracle (port of the reference's NumPy forward) on a bounded C3 sample."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import llama3_oracle as orc
+
+    try:
+        from threadpoolctl import threadpool_info
+
+        cores = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    except Exception:
+        cores = int(os.environ.get("OPENBLAS_NUM_THREADS", os.cpu_count() or 1))
+    Bs = 32
+    args = synth.stories15m(Bs)
+    w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=0)
+    model = orc.OracleModel(w, args)
+    ids = np.random.default_rng(1).integers(0, args.vocab_size, (Bs, SEQ))
+    model(ids[:4], 0)  # warm-up (small)
+    times = []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        model(ids, 0)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(cores),
+            "kind": "port",
+            "sample": f"oracle/llama3_oracle.py (NumPy restatement of the reference, f64 after layer-0 "
+                      f"RoPE as the reference) stories15M prefill B={Bs} L={SEQ}, median of 2 "
+                      f"({t:.2f} s each), OpenBLAS threads={cores}"}
+
+
+def traffic_per_launch():
+    p = os.path.join(REPO, "profiles", "pmc_gateup.json")
+    if not os.path.exists(p):
+        return None
+    with open(p) as f:
+        d = json.load(f)
+    if d.get("workload_rows") != B_PER_GPU * SEQ:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    dist = Dist(a.gpus)
+    dev = dist.local_rank
+    args = synth.stories15m(B_PER_GPU)
+    FD, D = synth.STORIES15M_HIDDEN, args.dim
+    weights = synth.make_weights(args, FD, seed=0)
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "stories15m_synth.npz")
+        synth.save_npz(path, weights)
+        model = llama3.Llama(path, args, device=dev)
+    ctx = model.context
+    VS = args.vocab_size
+
+    # inputs resident in HBM before the timed region
+    ids = np.random.default_rng(100 + dist.rank).integers(0, VS, (B_PER_GPU, SEQ)).astype(np.int32)
+    ids_dev = ctx.alloc(ids.nbytes)
+    ctx.h2d(ids_dev, ids)
+    logits_dev = ctx.alloc(B_PER_GPU * VS * 4)
+    gathered_dev = None
+    rows = [B_PER_GPU] * dist.world
+    if dist.world > 1:
+        uid = dist.bcast_bytes(l3hip.comm_unique_id() if dist.rank == 0 else None)
+        ctx.comm_init(dist.world, dist.rank, uid)
+        if dist.rank == 0:
+            gathered_dev = ctx.alloc(B_PER_GPU * dist.world * VS * 4)
+
+    def step():
+        ctx.forward_dev(ids_dev, B_PER_GPU, SEQ, 0, logits_dev)
+        if dist.world > 1:
+            ctx.gather_logits(logits_dev, gathered_dev, rows, root=0)
+
+    for _ in range(a.warmup):
+        step()
+    ctx.synchronize()
+
+    ctx.kernel_timing(True)  # HIP events around every launch, on the context stream
+    dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+    dist.barrier()
+    elapsed = dist.max(elapsed)
+    stats = ctx.kernel_stats()
+    ctx.kernel_timing(False)
+
+    # sanity on the output (outside the timed region)
+    probe = np.empty((2, VS), np.float32)
+    ctx.d2h(probe, logits_dev)
+    if not np.isfinite(probe).all():
+        raise SystemExit("non-finite logits")
+
+    if dist.rank != 0:
+        return
+    tokens = B_PER_GPU * SEQ * dist.world * a.steps
+    T = B_PER_GPU * SEQ
+    gu_ms, gu_n = stats["gateup"]
+    dn_ms, dn_n = stats["down"]
+    gu_flops = 2.0 * T * D * 2 * FD
+    dn_flops = 2.0 * T * FD * D
+    gu_avg_s = gu_ms / gu_n / 1e3
+    achieved = gu_flops / gu_avg_s / 1e12
+    ffn_tf = (gu_flops + dn_flops) / ((gu_ms / gu_n + dn_ms / dn_n) / 1e3) / 1e12
+    traffic = traffic_per_launch()
+    out = {
+        "metric": METRIC,
+        "value": round(tokens / elapsed, 1),
+        "unit": "tokens/s",
+        "n_gpus": dist.world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: stories15M-shaped N(0,0.02^2) weights (seed 0), uniform random ids",
+        "config": {"workload": f"stories15M prefill, B={B_PER_GPU} per GPU x L={SEQ}, start_pos 0",
+                   "global_batch": B_PER_GPU * dist.world, "seq_len": SEQ,
+                   "parallelism": f"dp{dist.world} (batch rows) + RCCL logits gather"},
+        "roofline": {"kernel": "gemm gate|up (fused SwiGLU epilogue), M=65536 K=288 N=1536",
+                     "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                     "traffic": traffic,
+                     "ffn": {"achieved": round(ffn_tf, 2),
+                             "frac": round(ffn_tf / PEAK_FP32_TFLOPS, 4)}},
+        "kernel_ms": {k: round(v[0] / v[1], 4) for k, v in stats.items() if v[1]},
+    }
+    if dist.world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/*
+ * llama3hip.h — C ABI of the MI355X (gfx950) forward pass for llama3.np.
+ *
+ * The reference (swap357/llama3.np) is pure NumPy and has no FFI; this ABI is
+ * what its Python classes bind to through ctypes (llama3.np_amd/l3hip.py).
+ * Each entry point names the reference interface it replaces (file:line in
+ * the reference repo).  Plain pointers and sizes only: no C++ or torch types.
+ *
+ * Conventions
+ *   - Every function returns 0 on success, non-zero on failure; the message is
+ *     in l3_last_error() (thread-local).  Nothing throws across the ABI.
+ *   - "_host" pointers are caller-owned host memory (C-contiguous); those
+ *     calls are synchronous.  "_dev" pointers are device memory from
+ *     l3_dev_alloc; those calls are asynchronous on the context's stream
+ *     (l3_synchronize waits).
+ *   - One context per device; a context is not re-entrant.
+ *   - All arithmetic is fp32 (the reference promotes to f64 after RoPE; parity
+ *     is to tolerance).
+ */
+#ifndef LLAMA3HIP_H
+#define LLAMA3HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct l3_ctx l3_ctx;
+
+/* Model shape; mirrors config.ModelArgs (reference config.py:5-19) plus the
+ * FeedForward hidden size, which the reference infers from the weights
+ * (llama3.py:89-95). */
+/* vocab_size 0 makes a layer-only context (standalone TransformerBlock /
+ * Attention); n_layers 0 makes an op-only context. */
+typedef struct l3_dims {
+    int32_t dim;            /* D */
+    int32_t n_layers;
+    int32_t n_heads;        /* H */
+    int32_t n_kv_heads;     /* KVH (already resolved: never "None") */
+    int32_t vocab_size;     /* VS */
+    int32_t hidden_dim;     /* FD */
+    int32_t max_seq_len;    /* M: KV-cache positions and RoPE table rows */
+    int32_t max_batch_size; /* KV-cache batch rows */
+    float norm_eps;
+} l3_dims;
+
+/* Weight kinds for l3_upload_weight; names follow the .npz keys the reference
+ * reads (llama3.py:219-237, 269, 280-281).  Shapes are the stored [out, in]. */
+enum l3_weight_kind {
+    L3_W_EMBED = 0,      /* model.embed_tokens.weight            [VS, D]        */
+    L3_W_Q = 1,          /* model.layers.i.self_attn.q_proj      [H*HD, D]      */
+    L3_W_K = 2,          /* ...k_proj                            [KVH*HD, D]    */
+    L3_W_V = 3,          /* ...v_proj                            [KVH*HD, D]    */
+    L3_W_O = 4,          /* ...o_proj                            [D, H*HD]      */
+    L3_W_GATE = 5,       /* model.layers.i.mlp.gate_proj         [FD, D]        */
+    L3_W_UP = 6,         /* ...up_proj                           [FD, D]        */
+    L3_W_DOWN = 7,       /* ...down_proj                         [D, FD]        */
+    L3_W_ATTN_NORM = 8,  /* model.layers.i.input_layernorm       [D]            */
+    L3_W_FFN_NORM = 9,   /* ...post_attention_layernorm          [D]            */
+    L3_W_FINAL_NORM = 10,/* model.norm.weight                    [D]            */
+    L3_W_LM_HEAD = 11    /* lm_head.weight                       [VS, D]        */
+};
+
+/* Kernel ids for l3_kernel_stats (per-kind HIP-event timing). */
+enum l3_kernel_id {
+    L3_K_EMBED = 0, L3_K_QKV = 1, L3_K_ATTN = 2, L3_K_OPROJ = 3, L3_K_GATEUP = 4,
+    L3_K_DOWN = 5, L3_K_LMHEAD = 6, L3_K_ARGMAX = 7, L3_K_GATHER = 8, L3_K_COUNT = 9
+};
+
+/* ---- errors / devices ---------------------------------------------------- */
+const char* l3_last_error(void);
+int l3_device_count(int32_t* n);
+int l3_version(int32_t* major, int32_t* minor);
+
+/* ---- context (replaces Llama.__init__, llama3.py:265-283) ---------------- */
+/* n_layers may be 0 (op-only context); ctx owns all device memory. */
+int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out);
+int l3_destroy(l3_ctx* ctx);
+/* Upload one tensor (host fp32, [rows, cols] row-major).  layer is ignored for
+ * EMBED/FINAL_NORM/LM_HEAD.  Replaces the weight.get(...) calls of
+ * TransformerBlock.__init__ (llama3.py:217-237) and Llama.__init__ (:269-281). */
+int l3_upload_weight(l3_ctx* ctx, int32_t layer, int32_t kind, const float* host,
+                     int64_t rows, int64_t cols);
+/* Mark the upload phase complete (QKV and gate/up are fused at upload time:
+ * q|k|v rows stacked, gate/up interleaved in 16-row groups).  Must be called
+ * once after the uploads, before any forward; entry points check that the
+ * tensors they need were uploaded. */
+int l3_finalize(l3_ctx* ctx);
+/* Zero every KV cache (the reference never does this; provided for reuse). */
+int l3_reset_cache(l3_ctx* ctx);
+
+/* ---- forward (replaces Llama.__call__, llama3.py:285-308) ----------------- */
+/* ids [B, L] int64 (host); logits_host [B, VS] fp32 = the reference's
+ * logits[:, 0, :].  Caches persist across calls, exactly as the reference's. */
+int l3_forward_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
+                    int32_t start_pos, float* logits_host);
+/* Same with device-resident ids (int32 [B, L]) and logits ([B, VS]); async. */
+int l3_forward_dev(l3_ctx* ctx, const int32_t* ids_dev, int32_t B, int32_t L,
+                   int32_t start_pos, float* logits_dev);
+/* One greedy step (Llama.generate body, llama3.py:313-320): forward + argmax
+ * (lowest index on ties, as np.argmax).  next_ids_host [B] int64;
+ * logits_host may be NULL. */
+int l3_greedy_step_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
+                        int32_t start_pos, int64_t* next_ids_host, float* logits_host);
+
+/* ---- one block (replaces TransformerBlock.__call__, llama3.py:239-261) --- */
+/* x [B, L, D] fp32 host -> out [B, L, D]; uses and updates layer's KV cache. */
+int l3_layer_forward_host(l3_ctx* ctx, int32_t layer, const float* x_host, int32_t B,
+                          int32_t L, int32_t start_pos, float* out_host);
+
+/* ---- one attention (replaces Attention.__call__, llama3.py:155-213) ------ */
+/* x [B, L, D] = the already-normalised block input; out [B, L, D] = O-projection
+ * output without residual.  Uses and updates the layer's KV cache. */
+int l3_attention_forward_host(l3_ctx* ctx, int32_t layer, const float* x_host, int32_t B,
+                              int32_t L, int32_t start_pos, float* out_host);
+
+/* ---- op-level entry points (reference module functions and classes) ------ */
+/* softmax over the last axis (llama3.py:22-24); rows x n. */
+int l3_op_softmax_host(l3_ctx* ctx, const float* x, int64_t rows, int64_t n, float* y);
+/* silu (llama3.py:27-28); n elements. */
+int l3_op_silu_host(l3_ctx* ctx, const float* x, int64_t n, float* y);
+/* RMSNorm (llama3.py:111-114); rows x dim. */
+int l3_op_rmsnorm_host(l3_ctx* ctx, const float* x, const float* w, int64_t rows,
+                       int64_t dim, float eps, float* y);
+/* apply_rotary_emb (llama3.py:41-76) on one tensor x [B, L, nh, HD] with fp32
+ * cos/sin tables [L, HD/2]. */
+int l3_op_rope_host(l3_ctx* ctx, const float* x, int32_t B, int32_t L, int32_t nh,
+                    int32_t hd, const float* cos_t, const float* sin_t, float* y);
+/* FeedForward.__call__ (llama3.py:97-103): x [rows, D], W as stored. */
+int l3_op_ffn_host(l3_ctx* ctx, const float* x, int64_t rows, int32_t dim, int32_t hidden,
+                   const float* w_gate, const float* w_up, const float* w_down, float* y);
+/* y [rows, N] = x [rows, K] @ W[N, K]^T (the reference's `x @ W.T`). */
+int l3_op_linear_host(l3_ctx* ctx, const float* x, int64_t rows, int32_t K, int32_t N,
+                      const float* w, float* y);
+
+/* ---- device memory helpers (bench: inputs resident in HBM) --------------- */
+int l3_dev_alloc(l3_ctx* ctx, size_t bytes, void** ptr);
+int l3_dev_free(l3_ctx* ctx, void* ptr);
+int l3_h2d(l3_ctx* ctx, void* dst_dev, const void* src_host, size_t bytes);
+int l3_d2h(l3_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
+int l3_synchronize(l3_ctx* ctx);
+
+/* ---- kernel timing (HIP events on the context stream) -------------------- */
+int l3_kernel_timing(l3_ctx* ctx, int32_t enable);    /* also resets the stats */
+/* total milliseconds and launch count per l3_kernel_id since last reset */
+int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
+
+/* ---- multi-GPU: batch-sharded prefill + RCCL logits gather (xGMI) -------- */
+/* 128-byte RCCL unique id (rank 0 creates, every rank receives it). */
+int l3_comm_unique_id(uint8_t id_out[128]);
+int l3_comm_init(l3_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+/* Gather each rank's logits rows [rows_r, VS] (device) into root's dst_dev
+ * [sum rows, VS] in rank order; rows_per_rank has nranks entries.  Async. */
+int l3_comm_gather_logits(l3_ctx* ctx, const float* src_dev, float* dst_dev,
+                          const int64_t* rows_per_rank, int32_t root);
+int l3_comm_barrier(l3_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LLAMA3HIP_H */

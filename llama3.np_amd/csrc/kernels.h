@@ -1,0 +1,52 @@
+// Internal kernel interface of libllama3hip (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace l3 {
+
+// Epilogues of the NT GEMM  C[M,N] = A[M,K] * W[N,K]^T  (see gemm.hip).
+enum Epilogue : int {
+    EPI_STORE = 0,   // C = s_row * acc
+    EPI_RESID = 1,   // C += acc                        (O-proj / down-proj + residual)
+    EPI_SWIGLU = 2,  // C[:, j] = silu(s*g_j) * (s*u_j) (gate/up interleaved by 16 rows)
+    EPI_QKV = 3,     // s_row * acc -> RoPE(q,k) -> q buffer + KV cache append
+};
+
+struct GemmArgs {
+    const float* A; int64_t lda;   // A rows, row stride (floats)
+    const float* W;                // [N, K] row-major
+    float* C; int64_t ldc;         // output (EPI_QKV: unused)
+    int M, N, K;
+    bool norm;                     // RMSNorm on A: A*norm_w, rows scaled by 1/sqrt(mean(A^2)+eps)
+    const float* norm_w;           // [K] (when norm)
+    float eps;
+    // EPI_QKV
+    float* q_out;                  // [M, H*HD], pre-scaled by q_scale
+    float* cache_k; float* cache_v;// [maxB, KVH, Smax, HD]
+    const float* rope_cos; const float* rope_sin;  // [Smax, HD/2]
+    int L, start_pos, H, KVH, HD, Smax;
+    float q_scale;
+};
+
+struct AttnArgs {
+    const float* q;       // [B*L, H*HD], pre-scaled by log2(e)/sqrt(HD)
+    const float* cache_k; // [maxB, KVH, Smax, HD]
+    const float* cache_v;
+    float* out;           // [B*L, H*HD]
+    int B, L, start_pos, H, KVH, HD, Smax;
+};
+
+hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
+hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
+hipError_t launch_embed(const int32_t* ids, const float* emb, float* h, int64_t T, int D,
+                        hipStream_t s);
+hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s);
+hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s);
+hipError_t launch_silu(const float* x, float* y, int64_t n, hipStream_t s);
+hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows, int dim,
+                          float eps, hipStream_t s);
+hipError_t launch_rope(const float* x, float* y, const float* cos_t, const float* sin_t, int B,
+                       int L, int nh, int hd, hipStream_t s);
+
+}  // namespace l3

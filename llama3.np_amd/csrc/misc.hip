@@ -1,0 +1,169 @@
+// Bandwidth-bound helper kernels for gfx950: embedding gather, greedy argmax, and the
+// op-level kernels behind the reference's module functions.  Loads are 16 B per lane where the layout allows (rows are multiples of 4 floats), one wavefront-wide
+// reduction per row for the row ops.
+#include "kernels.h"
+
+namespace l3 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// h[t, :] = emb[ids[t], :]   (llama3.py:287).  ids validated on the host.
+__global__ void embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ emb,
+                             float* __restrict__ h, int64_t T, int D4) {
+    const int64_t total = T * D4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = i / D4;
+        const int c = (int)(i - t * D4);
+        reinterpret_cast<f32x4*>(h)[i] = reinterpret_cast<const f32x4*>(emb)[(int64_t)ids[t] * D4 + c];
+    }
+}
+
+// argmax over each row with np.argmax's first-index tie-break (llama3.py:320).
+__global__ void argmax_kernel(const float* __restrict__ x, int n, int32_t* __restrict__ out) {
+    const float* row = x + (int64_t)blockIdx.x * n;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float v = row[i];
+        if (v > best || (v == best && i < bi) || (v != v && best == best)) { best = v; bi = i; }
+    }
+    __shared__ float sv[256];
+    __shared__ int si[256];
+    sv[threadIdx.x] = best;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) {
+            const float ov = sv[threadIdx.x + st];
+            const int oi = si[threadIdx.x + st];
+            const float cv = sv[threadIdx.x];
+            const int ci = si[threadIdx.x];
+            // NaN wins (np.argmax returns the first NaN), then larger value, then lower index
+            const bool onan = ov != ov, cnan = cv != cv;
+            bool take;
+            if (onan || cnan) take = onan && (!cnan || oi < ci);
+            else take = ov > cv || (ov == cv && oi < ci);
+            if (take) { sv[threadIdx.x] = ov; si[threadIdx.x] = oi; }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = si[0];
+}
+
+// row softmax (llama3.py:22-24): one wavefront per row, three passes over the row
+// (max, sum of exp, normalise); -inf entries give exact zeros.
+__global__ void softmax_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t rows,
+                               int n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + row * n;
+    float* yr = y + row * n;
+    float m = -INFINITY;
+    for (int i = lane; i < n; i += 64) m = fmaxf(m, xr[i]);
+    m = wave_max(m);
+    float s = 0.f;
+    for (int i = lane; i < n; i += 64) s += __expf(xr[i] - m);
+    s = wave_sum(s);
+    const float inv = 1.0f / s;
+    for (int i = lane; i < n; i += 64) yr[i] = __expf(xr[i] - m) * inv;
+}
+
+__global__ void silu_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = x[i];
+        y[i] = v * (1.0f / (1.0f + __expf(-v)));
+    }
+}
+
+// RMSNorm (llama3.py:111-114): one wavefront per row.
+__global__ void rmsnorm_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                               float* __restrict__ y, int64_t rows, int dim, float eps) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = blockIdx.x * (int64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (row >= rows) return;
+    const float* xr = x + row * dim;
+    float s = 0.f;
+    for (int i = lane; i < dim; i += 64) s += xr[i] * xr[i];
+    s = wave_sum(s);
+    const float inv = 1.0f / sqrtf(s / (float)dim + eps);
+    for (int i = lane; i < dim; i += 64) y[row * dim + i] = xr[i] * inv * w[i];
+}
+
+// interleaved-pair RoPE (llama3.py:41-76) on x [B, L, nh, hd] with tables [L, hd/2].
+__global__ void rope_kernel(const float* __restrict__ x, float* __restrict__ y,
+                            const float* __restrict__ cs, const float* __restrict__ sn, int B,
+                            int L, int nh, int hd) {
+    const int half = hd >> 1;
+    const int64_t pairs = (int64_t)B * L * nh * half;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < pairs;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(i % half);
+        const int64_t bl = i / ((int64_t)half * nh);
+        const int l = (int)(bl % L);
+        const float re = x[2 * i], im = x[2 * i + 1];
+        const float c = cs[l * half + k], s = sn[l * half + k];
+        y[2 * i] = re * c - im * s;
+        y[2 * i + 1] = re * s + im * c;
+    }
+}
+
+static inline unsigned grid_for(int64_t n, int block) {
+    int64_t g = (n + block - 1) / block;
+    if (g > 4096) g = 4096;
+    return (unsigned)(g < 1 ? 1 : g);
+}
+
+hipError_t launch_embed(const int32_t* ids, const float* emb, float* h, int64_t T, int D,
+                        hipStream_t s) {
+    if (D % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(embed_kernel, dim3(grid_for(T * (D / 4), 256)), dim3(256), 0, s, ids, emb, h,
+                       T, D / 4);
+    return hipGetLastError();
+}
+
+hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(256), 0, s, logits, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s) {
+    hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, y, rows,
+                       n);
+    return hipGetLastError();
+}
+
+hipError_t launch_silu(const float* x, float* y, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(silu_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, x, y, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows, int dim,
+                          float eps, hipStream_t s) {
+    hipLaunchKernelGGL(rmsnorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, w, y,
+                       rows, dim, eps);
+    return hipGetLastError();
+}
+
+hipError_t launch_rope(const float* x, float* y, const float* cos_t, const float* sin_t, int B,
+                       int L, int nh, int hd, hipStream_t s) {
+    if (hd % 2) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(rope_kernel, dim3(grid_for((int64_t)B * L * nh * (hd / 2), 256)), dim3(256),
+                       0, s, x, y, cos_t, sin_t, B, L, nh, hd);
+    return hipGetLastError();
+}
+
+}  // namespace l3

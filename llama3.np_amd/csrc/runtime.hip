@@ -1,0 +1,810 @@
+// libllama3hip runtime: device context, weight residency, forward orchestration, RCCL.
+// Implements include/llama3hip.h.  Reference anchors are given per entry point.
+//
+// Device layout (one context per GPU, everything resident in HBM for the context's life):
+//   emb        [VS, D]                       model.embed_tokens.weight
+//   per layer  wqkv [H*HD + 2*KVH*HD, D]     q|k|v rows stacked (one GEMM)
+//              wo   [D, H*HD]
+//              wgu  [2*FD, D]                gate/up interleaved in 16-row groups (one GEMM
+//                                            whose epilogue pairs gate_j with up_j)
+//              wd   [D, FD]
+//              n_attn / n_ffn [D]            RMSNorm weights, applied inside the GEMMs
+//              cache_k / cache_v [maxB, KVH, M, HD]  zero-initialised, persistent
+//   lm_head    [VS, D], final_norm [D]       (vocab_size 0: layer-only context, no tables)
+//   rope cos/sin [M, HD/2] fp32 (computed in double exactly as llama3.py:31-38, then rounded)
+//   workspace  h [T, D] residual stream, q [T, H*HD], attn [T, H*HD], hidden [T, FD],
+//              logits [B, VS], ids [T], argmax [B]   (grown on demand, T = B*L)
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/llama3hip.h"
+#include "kernels.h"
+
+using namespace l3;
+
+static thread_local std::string g_err;
+
+static int fail(const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return 1;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess)                                                            \
+            return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                       \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                         \
+    do {                                                                                       \
+        ncclResult_t r_ = (expr);                                                              \
+        if (r_ != ncclSuccess) return fail("%s failed: %s", #expr, ncclGetErrorString(r_));    \
+    } while (0)
+
+#define CHECK_CTX(ctx) \
+    if (!(ctx)) return fail("null context")
+
+struct Layer {
+    float* wqkv = nullptr;
+    float* wo = nullptr;
+    float* wgu = nullptr;
+    float* wd = nullptr;
+    float* n_attn = nullptr;
+    float* n_ffn = nullptr;
+    float* cache_k = nullptr;
+    float* cache_v = nullptr;
+    unsigned have = 0;  // bitmask of uploaded kinds
+};
+
+struct Timer {
+    hipEvent_t a, b;
+    int kind;
+};
+
+struct l3_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    l3_dims d{};
+    int HD = 0, qdim = 0, kvdim = 0, qkvn = 0;
+    float* emb = nullptr;
+    float* lm_head = nullptr;
+    float* final_norm = nullptr;
+    float* rope_cos = nullptr;
+    float* rope_sin = nullptr;
+    std::vector<Layer> layers;
+    bool have_emb = false, have_lm = false, have_fnorm = false, finalized = false;
+    // workspace
+    int64_t ws_T = 0, ws_B = 0;
+    float *h = nullptr, *q = nullptr, *attn = nullptr, *hid = nullptr, *logits = nullptr;
+    int32_t *ids = nullptr, *amax = nullptr;
+    // op scratch
+    std::vector<void*> scratch;
+    // timing
+    bool timing = false;
+    std::vector<Timer> timers;
+    size_t timer_used = 0;
+    double tot_ms[L3_K_COUNT] = {0};
+    int64_t cnt[L3_K_COUNT] = {0};
+    // rccl
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+// ---------------------------------------------------------------------------------------
+static int set_dev(l3_ctx* c) {
+    HIP_TRY(hipSetDevice(c->device));
+    return 0;
+}
+
+template <typename F>
+static int timed(l3_ctx* c, int kind, F&& launch) {
+    Timer* t = nullptr;
+    if (c->timing) {
+        if (c->timer_used == c->timers.size()) {
+            Timer nt{};
+            HIP_TRY(hipEventCreate(&nt.a));
+            HIP_TRY(hipEventCreate(&nt.b));
+            c->timers.push_back(nt);
+        }
+        t = &c->timers[c->timer_used++];
+        t->kind = kind;
+        HIP_TRY(hipEventRecord(t->a, c->stream));
+    }
+    hipError_t e = launch();
+    if (e != hipSuccess) return fail("kernel launch (kind %d) failed: %s", kind, hipGetErrorString(e));
+    if (t) HIP_TRY(hipEventRecord(t->b, c->stream));
+    return 0;
+}
+
+static int harvest_timers(l3_ctx* c) {
+    if (!c->timer_used) return 0;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i < c->timer_used; ++i) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->timers[i].a, c->timers[i].b));
+        c->tot_ms[c->timers[i].kind] += ms;
+        c->cnt[c->timers[i].kind] += 1;
+    }
+    c->timer_used = 0;
+    return 0;
+}
+
+static void dfree(void* p) {
+    if (p) (void)hipFree(p);
+}
+
+static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
+    const int64_t T = B * L;
+    if (T <= c->ws_T && B <= c->ws_B) return 0;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits);
+    dfree(c->ids); dfree(c->amax);
+    const int64_t Tn = T > c->ws_T ? T : c->ws_T;
+    const int64_t Bn = B > c->ws_B ? B : c->ws_B;
+    const int64_t D = c->d.dim;
+    HIP_TRY(hipMalloc(&c->h, Tn * D * 4));
+    HIP_TRY(hipMalloc(&c->q, Tn * c->qdim * 4));
+    HIP_TRY(hipMalloc(&c->attn, Tn * c->qdim * 4));
+    HIP_TRY(hipMalloc(&c->hid, Tn * (int64_t)c->d.hidden_dim * 4));
+    HIP_TRY(hipMalloc(&c->logits, Bn * (int64_t)c->d.vocab_size * 4));
+    HIP_TRY(hipMalloc(&c->ids, Tn * 4));
+    HIP_TRY(hipMalloc(&c->amax, Bn * 4));
+    c->ws_T = Tn;
+    c->ws_B = Bn;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
+
+extern "C" int l3_version(int32_t* major, int32_t* minor) {
+    if (major) *major = 0;
+    if (minor) *minor = 1;
+    return 0;
+}
+
+extern "C" int l3_device_count(int32_t* n) {
+    int k = 0;
+    HIP_TRY(hipGetDeviceCount(&k));
+    *n = k;
+    return 0;
+}
+
+extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
+    if (!dims || !out) return fail("l3_create: null argument");
+    const l3_dims& d = *dims;
+    if (d.dim <= 0 || d.n_heads <= 0 || d.n_kv_heads <= 0 || d.dim % d.n_heads)
+        return fail("l3_create: bad dims (dim %d, heads %d)", d.dim, d.n_heads);
+    if (d.n_heads % d.n_kv_heads) return fail("l3_create: n_heads %% n_kv_heads != 0");
+    const int HD = d.dim / d.n_heads;
+    if (d.n_layers > 0 && (HD % 16 || d.dim % 32 || d.hidden_dim % 32))
+        return fail("l3_create: need head_dim %% 16 == 0, dim %% 32 == 0, hidden %% 32 == 0 "
+                    "(got HD %d, D %d, FD %d)", HD, d.dim, d.hidden_dim);
+    if (d.n_layers > 0 && !(HD == 16 || HD == 48 || HD == 64 || HD == 128))
+        return fail("l3_create: head_dim %d has no attention instantiation", HD);
+    l3_ctx* c = new l3_ctx();
+    c->device = device;
+    c->d = d;
+    c->HD = HD;
+    c->qdim = d.n_heads * HD;
+    c->kvdim = d.n_kv_heads * HD;
+    c->qkvn = c->qdim + 2 * c->kvdim;
+    auto bail = [&](int rc) { l3_destroy(c); return rc; };
+    if (set_dev(c)) return bail(1);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail("hipStreamCreate failed"));
+    c->layers.resize(d.n_layers > 0 ? d.n_layers : 0);
+    if (d.n_layers > 0) {
+        const int64_t D = d.dim, FD = d.hidden_dim;
+        const int64_t cache = (int64_t)d.max_batch_size * d.n_kv_heads * d.max_seq_len * HD * 4;
+        for (auto& L : c->layers) {
+            if (hipMalloc(&L.wqkv, c->qkvn * D * 4) || hipMalloc(&L.wo, D * c->qdim * 4) ||
+                hipMalloc(&L.wgu, 2 * FD * D * 4) || hipMalloc(&L.wd, D * FD * 4) ||
+                hipMalloc(&L.n_attn, D * 4) || hipMalloc(&L.n_ffn, D * 4) ||
+                hipMalloc(&L.cache_k, cache) || hipMalloc(&L.cache_v, cache))
+                return bail(fail("l3_create: out of device memory (layers)"));
+            if (hipMemset(L.cache_k, 0, cache) || hipMemset(L.cache_v, 0, cache))
+                return bail(fail("l3_create: memset failed"));
+        }
+        const int64_t VD = (int64_t)d.vocab_size * D;
+        if (VD > 0 && (hipMalloc(&c->emb, VD * 4) || hipMalloc(&c->lm_head, VD * 4) ||
+                       hipMalloc(&c->final_norm, D * 4)))
+            return bail(fail("l3_create: out of device memory (embedding / lm_head)"));
+        // RoPE tables: llama3.py:31-38 in double, then fp32
+        const int half = HD / 2;
+        std::vector<float> cs((size_t)d.max_seq_len * half), sn(cs.size());
+        for (int t = 0; t < d.max_seq_len; ++t)
+            for (int i = 0; i < half; ++i) {
+                const double inv = 1.0 / std::pow(10000.0, (double)(2 * i) / (double)HD);
+                const double a = (double)t * inv;
+                cs[(size_t)t * half + i] = (float)std::cos(a);
+                sn[(size_t)t * half + i] = (float)std::sin(a);
+            }
+        if (hipMalloc(&c->rope_cos, cs.size() * 4) || hipMalloc(&c->rope_sin, sn.size() * 4) ||
+            hipMemcpy(c->rope_cos, cs.data(), cs.size() * 4, hipMemcpyHostToDevice) ||
+            hipMemcpy(c->rope_sin, sn.data(), sn.size() * 4, hipMemcpyHostToDevice))
+            return bail(fail("l3_create: rope table upload failed"));
+    }
+    *out = c;
+    return 0;
+}
+
+extern "C" int l3_destroy(l3_ctx* c) {
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    for (auto& L : c->layers) {
+        dfree(L.wqkv); dfree(L.wo); dfree(L.wgu); dfree(L.wd); dfree(L.n_attn); dfree(L.n_ffn);
+        dfree(L.cache_k); dfree(L.cache_v);
+    }
+    dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
+    dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
+    dfree(c->amax);
+    for (void* p : c->scratch) dfree(p);
+    for (auto& t : c->timers) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+static int expect_shape(int kind, int64_t rows, int64_t cols, int64_t er, int64_t ec) {
+    if (rows != er || cols != ec)
+        return fail("l3_upload_weight: kind %d has shape [%lld, %lld], expected [%lld, %lld]", kind,
+                    (long long)rows, (long long)cols, (long long)er, (long long)ec);
+    return 0;
+}
+
+extern "C" int l3_upload_weight(l3_ctx* c, int32_t layer, int32_t kind, const float* host,
+                                int64_t rows, int64_t cols) {
+    CHECK_CTX(c);
+    if (!host) return fail("l3_upload_weight: null host pointer");
+    if (c->finalized) return fail("l3_upload_weight: context already finalized");
+    if (set_dev(c)) return 1;
+    const int64_t D = c->d.dim, FD = c->d.hidden_dim, VS = c->d.vocab_size;
+    if ((kind == L3_W_EMBED || kind == L3_W_LM_HEAD || kind == L3_W_FINAL_NORM) && VS == 0)
+        return fail("l3_upload_weight: layer-only context (vocab_size 0) takes no kind %d", kind);
+    const bool per_layer = kind >= L3_W_Q && kind <= L3_W_FFN_NORM;
+    if (per_layer && (layer < 0 || layer >= (int)c->layers.size()))
+        return fail("l3_upload_weight: layer %d out of range [0, %d)", layer, (int)c->layers.size());
+    Layer* L = per_layer ? &c->layers[layer] : nullptr;
+    auto h2d = [&](float* dst, int64_t n) -> int {
+        HIP_TRY(hipMemcpy(dst, host, n * 4, hipMemcpyHostToDevice));
+        return 0;
+    };
+    switch (kind) {
+        case L3_W_EMBED:
+            if (expect_shape(kind, rows, cols, VS, D) || h2d(c->emb, VS * D)) return 1;
+            c->have_emb = true;
+            return 0;
+        case L3_W_LM_HEAD:
+            if (expect_shape(kind, rows, cols, VS, D) || h2d(c->lm_head, VS * D)) return 1;
+            c->have_lm = true;
+            return 0;
+        case L3_W_FINAL_NORM:
+            if (expect_shape(kind, rows, cols, 1, D) || h2d(c->final_norm, D)) return 1;
+            c->have_fnorm = true;
+            return 0;
+        case L3_W_Q:
+            if (expect_shape(kind, rows, cols, c->qdim, D) || h2d(L->wqkv, c->qdim * D)) return 1;
+            break;
+        case L3_W_K:
+            if (expect_shape(kind, rows, cols, c->kvdim, D) || h2d(L->wqkv + c->qdim * D, c->kvdim * D))
+                return 1;
+            break;
+        case L3_W_V:
+            if (expect_shape(kind, rows, cols, c->kvdim, D) ||
+                h2d(L->wqkv + (c->qdim + c->kvdim) * D, c->kvdim * D))
+                return 1;
+            break;
+        case L3_W_O:
+            if (expect_shape(kind, rows, cols, D, c->qdim) || h2d(L->wo, D * c->qdim)) return 1;
+            break;
+        case L3_W_GATE:
+        case L3_W_UP: {
+            if (expect_shape(kind, rows, cols, FD, D)) return 1;
+            // 16-row groups: fused row 32g + c <- gate row 16g + c, fused row 32g + 16 + c <- up
+            float* dst = L->wgu + (kind == L3_W_UP ? 16 * D : 0);
+            HIP_TRY(hipMemcpy2D(dst, 32 * D * 4, host, 16 * D * 4, 16 * D * 4, FD / 16,
+                                hipMemcpyHostToDevice));
+            break;
+        }
+        case L3_W_DOWN:
+            if (expect_shape(kind, rows, cols, D, FD) || h2d(L->wd, D * FD)) return 1;
+            break;
+        case L3_W_ATTN_NORM:
+            if (expect_shape(kind, rows, cols, 1, D) || h2d(L->n_attn, D)) return 1;
+            break;
+        case L3_W_FFN_NORM:
+            if (expect_shape(kind, rows, cols, 1, D) || h2d(L->n_ffn, D)) return 1;
+            break;
+        default:
+            return fail("l3_upload_weight: unknown kind %d", kind);
+    }
+    L->have |= 1u << kind;
+    return 0;
+}
+
+// Weight kinds each entry point needs (bit = l3_weight_kind).
+static const unsigned NEED_ATTN = (1u << L3_W_Q) | (1u << L3_W_K) | (1u << L3_W_V) | (1u << L3_W_O);
+static const unsigned NEED_LAYER = NEED_ATTN | (1u << L3_W_GATE) | (1u << L3_W_UP) |
+                                   (1u << L3_W_DOWN) | (1u << L3_W_ATTN_NORM) | (1u << L3_W_FFN_NORM);
+
+extern "C" int l3_finalize(l3_ctx* c) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    HIP_TRY(hipDeviceSynchronize());  // uploads were synchronous; keep the contract explicit
+    c->finalized = true;
+    return 0;
+}
+
+static int need_layer(l3_ctx* c, int li, unsigned mask) {
+    if ((c->layers[li].have & mask) != mask)
+        return fail("layer %d is missing weights (have 0x%x, need 0x%x)", li, c->layers[li].have, mask);
+    return 0;
+}
+
+static int need_model(l3_ctx* c) {
+    if (!c->have_emb || !c->have_lm || !c->have_fnorm)
+        return fail("model forward needs embedding, lm_head and final norm uploaded");
+    for (int i = 0; i < (int)c->layers.size(); ++i)
+        if (need_layer(c, i, NEED_LAYER)) return 1;
+    return 0;
+}
+
+extern "C" int l3_reset_cache(l3_ctx* c) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    const int64_t cache = (int64_t)c->d.max_batch_size * c->d.n_kv_heads * c->d.max_seq_len * c->HD * 4;
+    for (auto& L : c->layers) {
+        HIP_TRY(hipMemsetAsync(L.cache_k, 0, cache, c->stream));
+        HIP_TRY(hipMemsetAsync(L.cache_v, 0, cache, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+static int check_call(l3_ctx* c, int B, int L, int start_pos) {
+    if (!c->finalized) return fail("forward before l3_finalize");
+    if (B <= 0 || L <= 0) return fail("empty input: B=%d L=%d", B, L);
+    // the reference fails (broadcast error) in both cases: cache[:B] has max_batch_size rows
+    // (llama3.py:184) and freqs/cache slices stop at max_seq_len (:184, :289)
+    if (c->layers.empty()) return fail("op-only context has no layers");
+    if (B > c->d.max_batch_size)
+        return fail("batch %d exceeds max_batch_size %d", B, c->d.max_batch_size);
+    if (start_pos < 0 || start_pos + L > c->d.max_seq_len)
+        return fail("positions [%d, %d) exceed max_seq_len %d", start_pos, start_pos + L,
+                    c->d.max_seq_len);
+    return 0;
+}
+
+// one transformer block on the residual stream c->h [B*L, D] (llama3.py:239-261)
+static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos) {
+    Layer& Ly = c->layers[li];
+    const int64_t T = (int64_t)B * L;
+    const int D = c->d.dim, FD = c->d.hidden_dim;
+    GemmArgs g{};
+    g.eps = c->d.norm_eps;
+    // rmsnorm -> QKV -> RoPE -> q + KV-cache append
+    g.A = c->h; g.lda = D; g.W = Ly.wqkv; g.C = nullptr; g.ldc = 0;
+    g.M = (int)T; g.N = c->qkvn; g.K = D; g.norm = true; g.norm_w = Ly.n_attn;
+    g.q_out = c->q; g.cache_k = Ly.cache_k; g.cache_v = Ly.cache_v;
+    g.rope_cos = c->rope_cos; g.rope_sin = c->rope_sin;
+    g.L = L; g.start_pos = start_pos; g.H = c->d.n_heads; g.KVH = c->d.n_kv_heads; g.HD = c->HD;
+    g.Smax = c->d.max_seq_len;
+    g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
+    if (timed(c, L3_K_QKV, [&] { return launch_gemm(EPI_QKV, g, c->stream); })) return 1;
+    // causal attention over the cache
+    AttnArgs a{};
+    a.q = c->q; a.cache_k = Ly.cache_k; a.cache_v = Ly.cache_v; a.out = c->attn;
+    a.B = B; a.L = L; a.start_pos = start_pos; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
+    a.HD = c->HD; a.Smax = c->d.max_seq_len;
+    if (timed(c, L3_K_ATTN, [&] { return launch_attention(a, c->stream); })) return 1;
+    // O-proj + residual (in place on h)
+    GemmArgs o{};
+    o.A = c->attn; o.lda = c->qdim; o.W = Ly.wo; o.C = c->h; o.ldc = D;
+    o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
+    if (timed(c, L3_K_OPROJ, [&] { return launch_gemm(EPI_RESID, o, c->stream); })) return 1;
+    // rmsnorm -> gate|up -> SwiGLU
+    GemmArgs gu{};
+    gu.A = c->h; gu.lda = D; gu.W = Ly.wgu; gu.C = c->hid; gu.ldc = FD;
+    gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true; gu.norm_w = Ly.n_ffn;
+    gu.eps = c->d.norm_eps;
+    if (timed(c, L3_K_GATEUP, [&] { return launch_gemm(EPI_SWIGLU, gu, c->stream); })) return 1;
+    // down + residual
+    GemmArgs dn{};
+    dn.A = c->hid; dn.lda = FD; dn.W = Ly.wd; dn.C = c->h; dn.ldc = D;
+    dn.M = (int)T; dn.N = D; dn.K = FD; dn.norm = false;
+    if (timed(c, L3_K_DOWN, [&] { return launch_gemm(EPI_RESID, dn, c->stream); })) return 1;
+    return 0;
+}
+
+static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
+                       float* logits_dev) {
+    const int64_t T = (int64_t)B * L;
+    const int D = c->d.dim;
+    if (timed(c, L3_K_EMBED, [&] { return launch_embed(ids_dev, c->emb, c->h, T, D, c->stream); }))
+        return 1;
+    for (int li = 0; li < (int)c->layers.size(); ++li)
+        if (run_layer(c, li, B, L, start_pos)) return 1;
+    // final RMSNorm + lm_head on the last position of each sequence (llama3.py:304-307)
+    GemmArgs lm{};
+    lm.A = c->h + (int64_t)(L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
+    lm.C = logits_dev; lm.ldc = c->d.vocab_size;
+    lm.M = B; lm.N = c->d.vocab_size; lm.K = D; lm.norm = true; lm.norm_w = c->final_norm;
+    lm.eps = c->d.norm_eps;
+    if (timed(c, L3_K_LMHEAD, [&] { return launch_gemm(EPI_STORE, lm, c->stream); })) return 1;
+    return 0;
+}
+
+static int upload_ids(l3_ctx* c, const int64_t* ids_host, int64_t T) {
+    std::vector<int32_t> tmp((size_t)T);
+    const int64_t VS = c->d.vocab_size;
+    for (int64_t i = 0; i < T; ++i) {
+        int64_t v = ids_host[i];
+        if (v < -VS || v >= VS)  // NumPy fancy indexing raises IndexError here (llama3.py:287)
+            return fail("token id %lld out of range for vocab_size %lld", (long long)v, (long long)VS);
+        if (v < 0) v += VS;  // ...and wraps negatives
+        tmp[(size_t)i] = (int32_t)v;
+    }
+    HIP_TRY(hipMemcpyAsync(c->ids, tmp.data(), T * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));  // tmp goes out of scope
+    return 0;
+}
+
+extern "C" int l3_forward_dev(l3_ctx* c, const int32_t* ids_dev, int32_t B, int32_t L,
+                              int32_t start_pos, float* logits_dev) {
+    CHECK_CTX(c);
+    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
+    return forward_dev(c, ids_dev, B, L, start_pos, logits_dev);
+}
+
+extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
+                               int32_t start_pos, float* logits_host) {
+    CHECK_CTX(c);
+    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
+    if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
+    if (forward_dev(c, c->ids, B, L, start_pos, c->logits)) return 1;
+    HIP_TRY(hipMemcpyAsync(logits_host, c->logits, (int64_t)B * c->d.vocab_size * 4,
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
+                                   int32_t start_pos, int64_t* next_ids_host, float* logits_host) {
+    CHECK_CTX(c);
+    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
+    if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
+    if (forward_dev(c, c->ids, B, L, start_pos, c->logits)) return 1;
+    if (timed(c, L3_K_ARGMAX, [&] { return launch_argmax(c->logits, B, c->d.vocab_size, c->amax, c->stream); }))
+        return 1;
+    std::vector<int32_t> am((size_t)B);
+    HIP_TRY(hipMemcpyAsync(am.data(), c->amax, (int64_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+    if (logits_host)
+        HIP_TRY(hipMemcpyAsync(logits_host, c->logits, (int64_t)B * c->d.vocab_size * 4,
+                               hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < B; ++i) next_ids_host[i] = am[(size_t)i];
+    return 0;
+}
+
+extern "C" int l3_layer_forward_host(l3_ctx* c, int32_t layer, const float* x_host, int32_t B,
+                                     int32_t L, int32_t start_pos, float* out_host) {
+    CHECK_CTX(c);
+    if (layer < 0 || layer >= (int)c->layers.size()) return fail("layer %d out of range", layer);
+    if (need_layer(c, layer, NEED_LAYER) || check_call(c, B, L, start_pos) || set_dev(c) ||
+        ensure_ws(c, B, L))
+        return 1;
+    const int64_t n = (int64_t)B * L * c->d.dim;
+    HIP_TRY(hipMemcpyAsync(c->h, x_host, n * 4, hipMemcpyHostToDevice, c->stream));
+    if (run_layer(c, layer, B, L, start_pos)) return 1;
+    HIP_TRY(hipMemcpyAsync(out_host, c->h, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// Attention.__call__ (llama3.py:155-213): x is the already-normalised input; returns the
+// O-projection output (no residual).  Uses and updates the layer's KV cache.
+extern "C" int l3_attention_forward_host(l3_ctx* c, int32_t layer, const float* x_host, int32_t B,
+                                         int32_t L, int32_t start_pos, float* out_host) {
+    CHECK_CTX(c);
+    if (layer < 0 || layer >= (int)c->layers.size()) return fail("layer %d out of range", layer);
+    if (need_layer(c, layer, NEED_ATTN) || check_call(c, B, L, start_pos) || set_dev(c) ||
+        ensure_ws(c, B, L))
+        return 1;
+    Layer& Ly = c->layers[layer];
+    const int64_t T = (int64_t)B * L;
+    const int D = c->d.dim;
+    HIP_TRY(hipMemcpyAsync(c->h, x_host, T * D * 4, hipMemcpyHostToDevice, c->stream));
+    GemmArgs g{};
+    g.A = c->h; g.lda = D; g.W = Ly.wqkv; g.M = (int)T; g.N = c->qkvn; g.K = D; g.norm = false;
+    g.q_out = c->q; g.cache_k = Ly.cache_k; g.cache_v = Ly.cache_v;
+    g.rope_cos = c->rope_cos; g.rope_sin = c->rope_sin;
+    g.L = L; g.start_pos = start_pos; g.H = c->d.n_heads; g.KVH = c->d.n_kv_heads; g.HD = c->HD;
+    g.Smax = c->d.max_seq_len;
+    g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
+    if (timed(c, L3_K_QKV, [&] { return launch_gemm(EPI_QKV, g, c->stream); })) return 1;
+    AttnArgs a{};
+    a.q = c->q; a.cache_k = Ly.cache_k; a.cache_v = Ly.cache_v; a.out = c->attn;
+    a.B = B; a.L = L; a.start_pos = start_pos; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
+    a.HD = c->HD; a.Smax = c->d.max_seq_len;
+    if (timed(c, L3_K_ATTN, [&] { return launch_attention(a, c->stream); })) return 1;
+    GemmArgs o{};
+    o.A = c->attn; o.lda = c->qdim; o.W = Ly.wo; o.C = c->h; o.ldc = D;
+    o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
+    if (timed(c, L3_K_OPROJ, [&] { return launch_gemm(EPI_STORE, o, c->stream); })) return 1;
+    HIP_TRY(hipMemcpyAsync(out_host, c->h, T * D * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// op-level entry points: H2D -> kernel -> D2H on per-call scratch (not a hot path)
+struct Scratch {
+    l3_ctx* c;
+    std::vector<void*> ptrs;
+    ~Scratch() {
+        for (void* p : ptrs) dfree(p);
+    }
+    float* get(int64_t n) {
+        void* p = nullptr;
+        if (hipMalloc(&p, (size_t)(n > 0 ? n : 1) * 4) != hipSuccess) return nullptr;
+        ptrs.push_back(p);
+        return (float*)p;
+    }
+};
+
+#define SCRATCH(var, n)                                   \
+    float* var = S.get(n);                                \
+    if (!var) return fail("op scratch allocation failed")
+
+#define H2D(dst, src, n) HIP_TRY(hipMemcpyAsync(dst, src, (size_t)(n) * 4, hipMemcpyHostToDevice, c->stream))
+#define D2H(dst, src, n) HIP_TRY(hipMemcpyAsync(dst, src, (size_t)(n) * 4, hipMemcpyDeviceToHost, c->stream))
+
+extern "C" int l3_op_softmax_host(l3_ctx* c, const float* x, int64_t rows, int64_t n, float* y) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    Scratch S{c};
+    SCRATCH(dx, rows * n);
+    SCRATCH(dy, rows * n);
+    H2D(dx, x, rows * n);
+    HIP_TRY(launch_softmax(dx, dy, rows, (int)n, c->stream));
+    D2H(y, dy, rows * n);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_op_silu_host(l3_ctx* c, const float* x, int64_t n, float* y) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    Scratch S{c};
+    SCRATCH(dx, n);
+    SCRATCH(dy, n);
+    H2D(dx, x, n);
+    HIP_TRY(launch_silu(dx, dy, n, c->stream));
+    D2H(y, dy, n);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_op_rmsnorm_host(l3_ctx* c, const float* x, const float* w, int64_t rows,
+                                  int64_t dim, float eps, float* y) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    Scratch S{c};
+    SCRATCH(dx, rows * dim);
+    SCRATCH(dw, dim);
+    SCRATCH(dy, rows * dim);
+    H2D(dx, x, rows * dim);
+    H2D(dw, w, dim);
+    HIP_TRY(launch_rmsnorm(dx, dw, dy, rows, (int)dim, eps, c->stream));
+    D2H(y, dy, rows * dim);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_op_rope_host(l3_ctx* c, const float* x, int32_t B, int32_t L, int32_t nh,
+                               int32_t hd, const float* cos_t, const float* sin_t, float* y) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    const int64_t n = (int64_t)B * L * nh * hd, nt = (int64_t)L * (hd / 2);
+    Scratch S{c};
+    SCRATCH(dx, n);
+    SCRATCH(dy, n);
+    SCRATCH(dc, nt);
+    SCRATCH(ds, nt);
+    H2D(dx, x, n);
+    H2D(dc, cos_t, nt);
+    H2D(ds, sin_t, nt);
+    HIP_TRY(launch_rope(dx, dy, dc, ds, B, L, nh, hd, c->stream));
+    D2H(y, dy, n);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+static int op_linear(l3_ctx* c, int epi, const float* dA, int64_t rows, int K, int N,
+                     const float* dW, float* dC, bool norm) {
+    GemmArgs g{};
+    g.A = dA; g.lda = K; g.W = dW; g.C = dC; g.ldc = (epi == EPI_SWIGLU) ? N / 2 : N;
+    g.M = (int)rows; g.N = N; g.K = K; g.norm = norm;
+    HIP_TRY(launch_gemm(epi, g, c->stream));
+    return 0;
+}
+
+extern "C" int l3_op_linear_host(l3_ctx* c, const float* x, int64_t rows, int32_t K, int32_t N,
+                                 const float* w, float* y) {
+    CHECK_CTX(c);
+    if (K % 32) return fail("l3_op_linear: K=%d must be a multiple of 32", K);
+    if (set_dev(c)) return 1;
+    Scratch S{c};
+    SCRATCH(dx, rows * K);
+    SCRATCH(dw, (int64_t)N * K);
+    SCRATCH(dy, rows * N);
+    H2D(dx, x, rows * K);
+    H2D(dw, w, (int64_t)N * K);
+    if (op_linear(c, EPI_STORE, dx, rows, K, N, dw, dy, false)) return 1;
+    D2H(y, dy, rows * N);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_op_ffn_host(l3_ctx* c, const float* x, int64_t rows, int32_t dim, int32_t hidden,
+                              const float* w_gate, const float* w_up, const float* w_down, float* y) {
+    CHECK_CTX(c);
+    if (dim % 32 || hidden % 32) return fail("l3_op_ffn: dim and hidden must be multiples of 32");
+    if (set_dev(c)) return 1;
+    Scratch S{c};
+    SCRATCH(dx, rows * dim);
+    SCRATCH(dgu, 2LL * hidden * dim);
+    SCRATCH(dd, (int64_t)dim * hidden);
+    SCRATCH(dh, rows * hidden);
+    SCRATCH(dy, rows * dim);
+    H2D(dx, x, rows * dim);
+    HIP_TRY(hipMemcpy2DAsync(dgu, 32LL * dim * 4, w_gate, 16LL * dim * 4, 16LL * dim * 4, hidden / 16,
+                             hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpy2DAsync(dgu + 16LL * dim, 32LL * dim * 4, w_up, 16LL * dim * 4, 16LL * dim * 4,
+                             hidden / 16, hipMemcpyHostToDevice, c->stream));
+    H2D(dd, w_down, (int64_t)dim * hidden);
+    if (op_linear(c, EPI_SWIGLU, dx, rows, dim, 2 * hidden, dgu, dh, false)) return 1;
+    HIP_TRY(hipMemsetAsync(dy, 0, rows * dim * 4, c->stream));
+    if (op_linear(c, EPI_RESID, dh, rows, hidden, dim, dd, dy, false)) return 1;
+    D2H(y, dy, rows * dim);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+extern "C" int l3_dev_alloc(l3_ctx* c, size_t bytes, void** ptr) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    HIP_TRY(hipMalloc(ptr, bytes ? bytes : 4));
+    return 0;
+}
+extern "C" int l3_dev_free(l3_ctx* c, void* ptr) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipFree(ptr));
+    return 0;
+}
+extern "C" int l3_h2d(l3_ctx* c, void* dst, const void* src, size_t bytes) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+extern "C" int l3_d2h(l3_ctx* c, void* dst, const void* src, size_t bytes) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+extern "C" int l3_synchronize(l3_ctx* c) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_kernel_timing(l3_ctx* c, int32_t enable) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->timer_used = 0;
+    for (int k = 0; k < L3_K_COUNT; ++k) { c->tot_ms[k] = 0; c->cnt[k] = 0; }
+    c->timing = enable != 0;
+    return 0;
+}
+
+extern "C" int l3_kernel_stats(l3_ctx* c, double* total_ms, int64_t* count) {
+    CHECK_CTX(c);
+    if (set_dev(c) || harvest_timers(c)) return 1;
+    for (int k = 0; k < L3_K_COUNT; ++k) {
+        if (total_ms) total_ms[k] = c->tot_ms[k];
+        if (count) count[k] = c->cnt[k];
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+extern "C" int l3_comm_unique_id(uint8_t id_out[128]) {
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
+    memcpy(id_out, &id, 128);
+    return 0;
+}
+
+extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    ncclUniqueId uid;
+    memcpy(&uid, id, 128);
+    NCCL_TRY(ncclCommInitRank(&c->comm, nranks, uid, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return 0;
+}
+
+extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst_dev,
+                                     const int64_t* rows_per_rank, int32_t root) {
+    CHECK_CTX(c);
+    if (!c->comm) return fail("l3_comm_gather_logits: communicator not initialised");
+    if (set_dev(c)) return 1;
+    const int64_t VS = c->d.vocab_size;
+    // RCCL has no native gather: root posts one recv per peer, peers one send, all in one
+    // group so the point-to-point transfers run concurrently over the xGMI links.
+    NCCL_TRY(ncclGroupStart());
+    if (c->rank == root) {
+        int64_t off = 0;
+        for (int r = 0; r < c->nranks; ++r) {
+            const int64_t n = rows_per_rank[r] * VS;
+            if (r == root) {
+                if (n && dst_dev + off * VS != src_dev)
+                    HIP_TRY(hipMemcpyAsync(dst_dev + off * VS, src_dev, n * 4, hipMemcpyDeviceToDevice,
+                                           c->stream));
+            } else if (n) {
+                NCCL_TRY(ncclRecv(dst_dev + off * VS, (size_t)n, ncclFloat32, r, c->comm, c->stream));
+            }
+            off += rows_per_rank[r];
+        }
+    } else if (rows_per_rank[c->rank]) {
+        NCCL_TRY(ncclSend(src_dev, (size_t)(rows_per_rank[c->rank] * VS), ncclFloat32, root, c->comm,
+                          c->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return 0;
+}
+
+extern "C" int l3_comm_barrier(l3_ctx* c) {
+    CHECK_CTX(c);
+    if (!c->comm) return fail("l3_comm_barrier: communicator not initialised");
+    if (set_dev(c)) return 1;
+    float* one = nullptr;
+    if (!c->scratch.empty()) one = (float*)c->scratch[0];
+    else {
+        HIP_TRY(hipMalloc(&one, 4));
+        c->scratch.push_back(one);
+    }
+    NCCL_TRY(ncclAllReduce(one, one, 1, ncclFloat32, ncclSum, c->comm, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}

@@ -1,0 +1,299 @@
+"""ctypes binding to libllama3hip.so (C ABI: include/llama3hip.h).
+
+This is the only module that touches the native library.  It has no CPU
+fallback: if the shared library is missing, ``lib()`` raises, and every device
+entry point raises ``RuntimeError(l3_last_error())`` on a non-zero return.
+Loading the library needs no GPU (it only resolves symbols); calling a compute
+entry point without a HIP device fails loudly.
+"""
+
+import ctypes
+import os
+import re
+from typing import List, Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "csrc", "libllama3hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "llama3hip.h")
+
+# weight kinds / kernel ids (mirror the enums in include/llama3hip.h)
+W_EMBED, W_Q, W_K, W_V, W_O, W_GATE, W_UP, W_DOWN = range(8)
+W_ATTN_NORM, W_FFN_NORM, W_FINAL_NORM, W_LM_HEAD = 8, 9, 10, 11
+KERNELS = ["embed", "qkv", "attn", "oproj", "gateup", "down", "lmhead", "argmax", "gather"]
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [
+        ("dim", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("n_heads", ctypes.c_int32),
+        ("n_kv_heads", ctypes.c_int32),
+        ("vocab_size", ctypes.c_int32),
+        ("hidden_dim", ctypes.c_int32),
+        ("max_seq_len", ctypes.c_int32),
+        ("max_batch_size", ctypes.c_int32),
+        ("norm_eps", ctypes.c_float),
+    ]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_SZ = ctypes.c_size_t
+_F = ctypes.c_float
+
+_SIGNATURES = {
+    "l3_last_error": (ctypes.c_char_p, []),
+    "l3_device_count": (ctypes.c_int, [_P]),
+    "l3_version": (ctypes.c_int, [_P, _P]),
+    "l3_create": (ctypes.c_int, [_I32, _P, _P]),
+    "l3_destroy": (ctypes.c_int, [_P]),
+    "l3_upload_weight": (ctypes.c_int, [_P, _I32, _I32, _P, _I64, _I64]),
+    "l3_finalize": (ctypes.c_int, [_P]),
+    "l3_reset_cache": (ctypes.c_int, [_P]),
+    "l3_forward_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
+    "l3_forward_dev": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
+    "l3_greedy_step_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
+    "l3_layer_forward_host": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P]),
+    "l3_attention_forward_host": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P]),
+    "l3_op_softmax_host": (ctypes.c_int, [_P, _P, _I64, _I64, _P]),
+    "l3_op_silu_host": (ctypes.c_int, [_P, _P, _I64, _P]),
+    "l3_op_rmsnorm_host": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _F, _P]),
+    "l3_op_rope_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
+    "l3_op_ffn_host": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P, _P, _P]),
+    "l3_op_linear_host": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P, _P]),
+    "l3_dev_alloc": (ctypes.c_int, [_P, _SZ, _P]),
+    "l3_dev_free": (ctypes.c_int, [_P, _P]),
+    "l3_h2d": (ctypes.c_int, [_P, _P, _P, _SZ]),
+    "l3_d2h": (ctypes.c_int, [_P, _P, _P, _SZ]),
+    "l3_synchronize": (ctypes.c_int, [_P]),
+    "l3_kernel_timing": (ctypes.c_int, [_P, _I32]),
+    "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
+    "l3_comm_unique_id": (ctypes.c_int, [_P]),
+    "l3_comm_init": (ctypes.c_int, [_P, _I32, _I32, _P]),
+    "l3_comm_gather_logits": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
+    "l3_comm_barrier": (ctypes.c_int, [_P]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the HIP library (built by ``__graft_entry__.build()`` / ``make -C csrc``)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libllama3hip.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        so = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(so, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = so
+    return _lib
+
+
+def header_symbols() -> List[str]:
+    """Every function the public header declares (used by the ABI test)."""
+    with open(HEADER) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(l3_\w+)\s*\(", text, re.M)))
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError("libllama3hip: " + lib().l3_last_error().decode(errors="replace"))
+
+
+def ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def device_count() -> int:
+    n = ctypes.c_int32(0)
+    check(lib().l3_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class Context:
+    """Owns one device context (weights, KV caches, workspace) on one GPU."""
+
+    def __init__(self, dims: Dims, device: int = 0):
+        self._h = ctypes.c_void_p()
+        check(lib().l3_create(device, ctypes.byref(dims), ctypes.byref(self._h)))
+        self.dims = dims
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().l3_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- weights ----
+    def upload(self, layer: int, kind: int, w: np.ndarray) -> None:
+        a = np.ascontiguousarray(w, dtype=np.float32)
+        rows, cols = (1, a.shape[0]) if a.ndim == 1 else a.shape
+        check(lib().l3_upload_weight(self._h, layer, kind, ptr(a), rows, cols))
+
+    def finalize(self) -> None:
+        check(lib().l3_finalize(self._h))
+
+    def reset_cache(self) -> None:
+        check(lib().l3_reset_cache(self._h))
+
+    # ---- forward ----
+    def forward(self, ids: np.ndarray, start_pos: int) -> np.ndarray:
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        B, L = ids.shape
+        out = np.empty((B, self.dims.vocab_size), np.float32)
+        check(lib().l3_forward_host(self._h, ptr(ids), B, L, start_pos, ptr(out)))
+        return out
+
+    def greedy_step(self, ids: np.ndarray, start_pos: int, want_logits: bool = False):
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        B, L = ids.shape
+        nxt = np.empty(B, np.int64)
+        logits = np.empty((B, self.dims.vocab_size), np.float32) if want_logits else None
+        check(lib().l3_greedy_step_host(self._h, ptr(ids), B, L, start_pos, ptr(nxt),
+                                        ptr(logits) if logits is not None else None))
+        return nxt, logits
+
+    def layer_forward(self, layer: int, x: np.ndarray, start_pos: int) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        B, L, _ = x.shape
+        out = np.empty_like(x)
+        check(lib().l3_layer_forward_host(self._h, layer, ptr(x), B, L, start_pos, ptr(out)))
+        return out
+
+    def attention_forward(self, layer: int, x: np.ndarray, start_pos: int) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        B, L, _ = x.shape
+        out = np.empty_like(x)
+        check(lib().l3_attention_forward_host(self._h, layer, ptr(x), B, L, start_pos, ptr(out)))
+        return out
+
+    # ---- device buffers (bench) ----
+    def alloc(self, nbytes: int) -> int:
+        p = ctypes.c_void_p()
+        check(lib().l3_dev_alloc(self._h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def free(self, p: int) -> None:
+        check(lib().l3_dev_free(self._h, p))
+
+    def h2d(self, dst: int, a: np.ndarray) -> None:
+        a = np.ascontiguousarray(a)
+        check(lib().l3_h2d(self._h, dst, ptr(a), a.nbytes))
+
+    def d2h(self, a: np.ndarray, src: int) -> np.ndarray:
+        check(lib().l3_d2h(self._h, ptr(a), src, a.nbytes))
+        return a
+
+    def forward_dev(self, ids_dev: int, B: int, L: int, start_pos: int, logits_dev: int) -> None:
+        check(lib().l3_forward_dev(self._h, ids_dev, B, L, start_pos, logits_dev))
+
+    def synchronize(self) -> None:
+        check(lib().l3_synchronize(self._h))
+
+    def kernel_timing(self, enable: bool) -> None:
+        check(lib().l3_kernel_timing(self._h, 1 if enable else 0))
+
+    def kernel_stats(self) -> dict:
+        ms = np.zeros(len(KERNELS), np.float64)
+        cnt = np.zeros(len(KERNELS), np.int64)
+        check(lib().l3_kernel_stats(self._h, ptr(ms), ptr(cnt)))
+        return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(KERNELS)}
+
+    # ---- RCCL ----
+    def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().l3_comm_init(self._h, nranks, rank, buf))
+
+    def gather_logits(self, src_dev: int, dst_dev: Optional[int], rows_per_rank, root: int = 0):
+        rows = np.ascontiguousarray(rows_per_rank, dtype=np.int64)
+        check(lib().l3_comm_gather_logits(self._h, src_dev, dst_dev or 0, ptr(rows), root))
+
+    def comm_barrier(self) -> None:
+        check(lib().l3_comm_barrier(self._h))
+
+    # ---- ops ----
+    def op_softmax(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        y = np.empty_like(x)
+        n = x.shape[-1]
+        check(lib().l3_op_softmax_host(self._h, ptr(x), x.size // n, n, ptr(y)))
+        return y
+
+    def op_silu(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        y = np.empty_like(x)
+        check(lib().l3_op_silu_host(self._h, ptr(x), x.size, ptr(y)))
+        return y
+
+    def op_rmsnorm(self, x: np.ndarray, w: np.ndarray, eps: float) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        y = np.empty_like(x)
+        n = x.shape[-1]
+        check(lib().l3_op_rmsnorm_host(self._h, ptr(x), ptr(w), x.size // n, n, eps, ptr(y)))
+        return y
+
+    def op_rope(self, x: np.ndarray, cos_t: np.ndarray, sin_t: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        c = np.ascontiguousarray(cos_t, dtype=np.float32)
+        s = np.ascontiguousarray(sin_t, dtype=np.float32)
+        B, L, nh, hd = x.shape
+        y = np.empty_like(x)
+        check(lib().l3_op_rope_host(self._h, ptr(x), B, L, nh, hd, ptr(c), ptr(s), ptr(y)))
+        return y
+
+    def op_linear(self, x: np.ndarray, w: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        K = x.shape[-1]
+        N = w.shape[0]
+        y = np.empty(x.shape[:-1] + (N,), np.float32)
+        check(lib().l3_op_linear_host(self._h, ptr(x), x.size // K, K, N, ptr(w), ptr(y)))
+        return y
+
+    def op_ffn(self, x: np.ndarray, wg: np.ndarray, wu: np.ndarray, wd: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        D = x.shape[-1]
+        FD = wg.shape[0]
+        y = np.empty_like(x)
+        wg, wu, wd = (np.ascontiguousarray(a, dtype=np.float32) for a in (wg, wu, wd))
+        check(lib().l3_op_ffn_host(self._h, ptr(x), x.size // D, D, FD, ptr(wg), ptr(wu), ptr(wd),
+                                   ptr(y)))
+        return y
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * 128)()
+    check(lib().l3_comm_unique_id(buf))
+    return bytes(buf)
+
+
+_op_ctx = {}
+
+
+def op_context(device: int = 0) -> Context:
+    """Shared op-only context (n_layers = 0) used by the module-level ops."""
+    if device not in _op_ctx:
+        d = Dims(dim=64, n_layers=0, n_heads=1, n_kv_heads=1, vocab_size=1, hidden_dim=32,
+                 max_seq_len=1, max_batch_size=1, norm_eps=1e-6)
+        _op_ctx[device] = Context(d, device)
+    return _op_ctx[device]

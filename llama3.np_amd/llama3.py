@@ -1,0 +1,282 @@
+"""MI355X drop-in for the reference's ``llama3.py`` (swap357/llama3.np).
+
+Same public surface — ``Llama``, ``TransformerBlock``, ``Attention``,
+``FeedForward``, ``RMSNorm``, ``softmax``, ``silu``, ``compute_cos_sin_cache``,
+``apply_rotary_emb``, ``repeat_kv`` and the ``__main__`` CLI — with the
+arithmetic executed by hand-written gfx950 HIP kernels through the C ABI in
+``include/llama3hip.h`` (``l3hip.py``).  There is no NumPy fallback: without
+``libllama3hip.so`` or without a HIP device every compute call raises.
+
+Differences from the reference, all deliberate:
+
+* arithmetic is fp32 everywhere (the reference promotes to f64 after RoPE,
+  ``llama3.py:181``, via its f64 tables and caches); logits are returned as
+  float32 ``[B, 1, VS]``.  Parity is to tolerance.
+* ``TransformerBlock.__call__`` / ``Attention.__call__`` accept ``mask`` and
+  ``freqs_cos/freqs_sin`` for signature compatibility but rebuild the causal
+  mask and RoPE angles on the device from ``(start_pos, L)`` — the reference's
+  callers always pass exactly those (``llama3.py:289-297``); shapes are checked.
+* ``compute_cos_sin_cache`` stays a host function (init-time f64 tables, as
+  ``llama3.py:31-38``); the device builds its own fp32 copy of the same table.
+
+Everything the reference keeps on the object (``args``, ``tok_embedding``,
+``freqs_cos/sin``, ``layers``, ``norm``, ``lm_head_weight``, per-class weight
+views) is kept, so introspecting code keeps working.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import time
+from typing import Iterator, Optional
+
+import numpy as np
+
+import l3hip
+from config import ModelArgs
+from tokenizer import Tokenizer
+from utils import load_parameters
+
+DEFAULT_DEVICE = int(os.environ.get("LLAMA3_HIP_DEVICE", "0"))
+
+
+# ---- module functions (reference llama3.py:22-83) ----------------------------
+
+def softmax(x):
+    """Row softmax over the last axis on the GPU (reference llama3.py:22-24)."""
+    x = np.asarray(x)
+    return l3hip.op_context(DEFAULT_DEVICE).op_softmax(x).reshape(x.shape)
+
+
+def silu(x):
+    """x * sigmoid(x) on the GPU (reference llama3.py:27-28)."""
+    x = np.asarray(x)
+    return l3hip.op_context(DEFAULT_DEVICE).op_silu(x).reshape(x.shape)
+
+
+def compute_cos_sin_cache(head_dim: int, max_seq_len: int, base: int = 10000):
+    """Host f64 RoPE tables, same formula as reference llama3.py:31-38."""
+    inv_freq = 1.0 / (base ** (np.arange(0, head_dim, 2)[: head_dim // 2] / head_dim))
+    ang = np.outer(np.arange(max_seq_len), inv_freq)
+    return np.cos(ang), np.sin(ang)
+
+
+def apply_rotary_emb(xq, xk, freqs_cos, freqs_sin):
+    """Interleaved-pair RoPE of q and k on the GPU (reference llama3.py:41-76)."""
+    ctx = l3hip.op_context(DEFAULT_DEVICE)
+    return ctx.op_rope(xq, freqs_cos, freqs_sin), ctx.op_rope(xk, freqs_cos, freqs_sin)
+
+
+def repeat_kv(x, n_rep: int):
+    """GQA head expansion (reference llama3.py:79-83).
+
+    Pure data movement; inside the device forward the expansion is an index
+    map (query head h reads KV head h // n_rep), never a copy."""
+    if n_rep == 1:
+        return x
+    return np.repeat(x, n_rep, axis=2)
+
+
+# ---- layers ------------------------------------------------------------------
+
+def _dims(args: ModelArgs, hidden_dim: int, n_layers: int, vocab_size: int) -> l3hip.Dims:
+    kvh = args.n_heads if args.n_kv_heads is None else args.n_kv_heads
+    return l3hip.Dims(dim=args.dim, n_layers=n_layers, n_heads=args.n_heads, n_kv_heads=kvh,
+                      vocab_size=vocab_size, hidden_dim=hidden_dim, max_seq_len=args.max_seq_len,
+                      max_batch_size=args.max_batch_size, norm_eps=args.norm_eps)
+
+
+def _check_freqs(freqs_cos, freqs_sin, L: int, head_dim: int) -> None:
+    for f in (freqs_cos, freqs_sin):
+        if f is not None and np.shape(f) != (L, head_dim // 2):
+            raise ValueError(f"freqs shape {np.shape(f)} does not match (L={L}, HD/2={head_dim // 2})")
+
+
+class FeedForward:
+    """SwiGLU MLP (reference llama3.py:86-103): one fused gate|up MFMA GEMM with a
+    silu(g)*u epilogue, then the down GEMM."""
+
+    def __init__(self, up_weight, gate_weight, down_weight):
+        self.up_weight = up_weight.T
+        self.gate_weight = gate_weight.T
+        self.down_weight = down_weight.T
+
+    def __call__(self, x):
+        x = np.asarray(x)
+        ctx = l3hip.op_context(DEFAULT_DEVICE)
+        y = ctx.op_ffn(x.reshape(-1, x.shape[-1]), self.gate_weight.T, self.up_weight.T,
+                       self.down_weight.T)
+        return y.reshape(x.shape)
+
+
+class RMSNorm:
+    """x / sqrt(mean(x^2) + eps) * w (reference llama3.py:106-114)."""
+
+    def __init__(self, weight, eps: float):
+        self.weight = weight
+        self.eps = eps
+
+    def __call__(self, x):
+        x = np.asarray(x)
+        return l3hip.op_context(DEFAULT_DEVICE).op_rmsnorm(x, self.weight, self.eps).reshape(x.shape)
+
+
+class Attention:
+    """Causal GQA attention with a persistent device KV cache (reference llama3.py:117-213).
+
+    Owned by a ``TransformerBlock`` it shares that block's device state
+    (cache included), exactly as the reference's Attention owns the cache the
+    block uses.  Constructed alone it gets a private one-layer context."""
+
+    def __init__(self, q_weight, k_weight, v_weight, o_weight, args: ModelArgs,
+                 _bind: Optional[tuple] = None):
+        self.n_kv_heads = args.n_heads if args.n_kv_heads is None else args.n_kv_heads
+        assert args.n_heads % self.n_kv_heads == 0
+        self.n_local_heads = args.n_heads
+        self.n_local_kv_heads = self.n_kv_heads
+        self.n_rep = self.n_local_heads // self.n_local_kv_heads
+        self.head_dim = args.dim // args.n_heads
+        self.q_weight = q_weight.T
+        self.k_weight = k_weight.T
+        self.v_weight = v_weight.T
+        self.o_weight = o_weight.T
+        if _bind is None:
+            ctx = l3hip.Context(_dims(args, 32, 1, 0), DEFAULT_DEVICE)
+            for kind, w in ((l3hip.W_Q, q_weight), (l3hip.W_K, k_weight), (l3hip.W_V, v_weight),
+                            (l3hip.W_O, o_weight)):
+                ctx.upload(0, kind, w)
+            ctx.finalize()
+            _bind = (ctx, 0)
+        self._ctx, self._layer = _bind
+
+    def __call__(self, x, start_pos: int, mask, freqs_cos, freqs_sin):
+        x = np.asarray(x)
+        _check_freqs(freqs_cos, freqs_sin, x.shape[1], self.head_dim)
+        return self._ctx.attention_forward(self._layer, x, start_pos)
+
+
+class TransformerBlock:
+    """Pre-norm block (reference llama3.py:216-261) executed as 4 MFMA GEMMs with
+    fused epilogues plus one fused attention kernel (kernel list)."""
+
+    def __init__(self, weight: dict, layer_id: int, args: ModelArgs, _bind: Optional[tuple] = None):
+        p = f"model.layers.{layer_id}."
+        names = {
+            l3hip.W_Q: p + "self_attn.q_proj.weight", l3hip.W_K: p + "self_attn.k_proj.weight",
+            l3hip.W_V: p + "self_attn.v_proj.weight", l3hip.W_O: p + "self_attn.o_proj.weight",
+            l3hip.W_GATE: p + "mlp.gate_proj.weight", l3hip.W_UP: p + "mlp.up_proj.weight",
+            l3hip.W_DOWN: p + "mlp.down_proj.weight",
+            l3hip.W_ATTN_NORM: p + "input_layernorm.weight",
+            l3hip.W_FFN_NORM: p + "post_attention_layernorm.weight",
+        }
+        w = {}
+        for kind, name in names.items():
+            t = weight.get(name)
+            if t is None:  # the reference fails later with AttributeError on None.T
+                raise KeyError(f"missing weight {name!r}")
+            w[kind] = t
+        if _bind is None:
+            ctx = l3hip.Context(_dims(args, w[l3hip.W_GATE].shape[0], 1, 0), DEFAULT_DEVICE)
+            _bind = (ctx, 0)
+            standalone = True
+        else:
+            standalone = False
+        self._ctx, self._layer = _bind
+        for kind, t in w.items():
+            self._ctx.upload(self._layer, kind, t)
+        if standalone:
+            self._ctx.finalize()
+        self.attention = Attention(w[l3hip.W_Q], w[l3hip.W_K], w[l3hip.W_V], w[l3hip.W_O], args,
+                                   _bind=_bind)
+        self.feed_forward = FeedForward(w[l3hip.W_UP], w[l3hip.W_GATE], w[l3hip.W_DOWN])
+        self.input_layernorm = RMSNorm(w[l3hip.W_ATTN_NORM], eps=args.norm_eps)
+        self.post_attention_layernorm = RMSNorm(w[l3hip.W_FFN_NORM], eps=args.norm_eps)
+        self._head_dim = args.dim // args.n_heads
+
+    def __call__(self, x, start_pos: int, mask, freqs_cos, freqs_sin):
+        x = np.asarray(x)
+        _check_freqs(freqs_cos, freqs_sin, x.shape[1], self._head_dim)
+        return self._ctx.layer_forward(self._layer, x, start_pos)
+
+
+class Llama:
+    """The whole forward + greedy loop (reference llama3.py:264-321).
+
+    Weights are uploaded once to HBM; ``__call__`` keeps activations
+    device-resident across all layers and copies back only the last-position
+    logits.  ``generate`` runs argmax on the device and copies back only ids."""
+
+    def __init__(self, model_path: str, args: ModelArgs, device: Optional[int] = None):
+        self.args = args
+        weight = load_parameters(model_path)
+        self.tok_embedding = weight.get("model.embed_tokens.weight")
+        self.freqs_cos, self.freqs_sin = compute_cos_sin_cache(args.dim // args.n_heads,
+                                                               args.max_seq_len)
+        hidden = weight.get("model.layers.0.mlp.gate_proj.weight").shape[0]
+        dev = DEFAULT_DEVICE if device is None else device
+        self._ctx = l3hip.Context(_dims(args, hidden, args.n_layers, args.vocab_size), dev)
+        self._ctx.upload(0, l3hip.W_EMBED, self.tok_embedding)
+        self.layers = [TransformerBlock(weight, i, args, _bind=(self._ctx, i))
+                       for i in range(args.n_layers)]
+        self.norm = RMSNorm(weight.get("model.norm.weight"), eps=args.norm_eps)
+        lm = weight.get("lm_head.weight")
+        self.lm_head_weight = lm.T
+        self._ctx.upload(0, l3hip.W_FINAL_NORM, self.norm.weight)
+        self._ctx.upload(0, l3hip.W_LM_HEAD, lm)
+        self._ctx.finalize()
+        del weight
+
+    @property
+    def context(self) -> l3hip.Context:
+        return self._ctx
+
+    def __call__(self, input_ids, start_pos: int):
+        ids = np.asarray(input_ids)
+        if ids.ndim != 2:
+            raise ValueError(f"input_ids must be [B, L], got shape {ids.shape}")
+        logits = self._ctx.forward(ids, int(start_pos))
+        return logits[:, None, :]
+
+    def generate(self, input_ids, max_new_tokens: int) -> Iterator[np.ndarray]:
+        """Greedy decode with the reference's exact position schedule
+        (llama3.py:310-321): prefill at 0, then decode step i >= 1 at pos = L + i,
+        so KV slot L is never written and stays zero (the "decode hole")."""
+        ids = np.asarray(input_ids)
+        _, L = ids.shape
+        next_id = None
+        for i, curr_pos in enumerate(range(L, max_new_tokens)):
+            if i == 0:
+                nxt, _ = self._ctx.greedy_step(ids, 0)
+            else:
+                nxt, _ = self._ctx.greedy_step(next_id, curr_pos)
+            next_id = nxt.reshape(-1, 1)
+            yield next_id
+
+
+def main(argv=None, tokenizer_path="./tokenizer.model.np", model_path="./stories15M.model.npz"):
+    """CLI of reference llama3.py:324-349: stream greedy tokens for a prompt, stop on
+    EOS/BOS, then print the reference's counter line (prompt + generated tokens
+    over wall time including prefill)."""
+    argv = sys.argv[1:] if argv is None else argv
+    prompt = argv[0] if argv else "I have a dream"
+    args = ModelArgs()
+    tok = Tokenizer(tokenizer_path)
+    model = Llama(model_path, args)
+    print(f"\n{prompt}", end="")
+    ids = np.array([tok.encode(prompt)])
+    count = ids.shape[1]
+    t0 = time.time()
+    for step in model.generate(ids, args.max_new_tokens):
+        count += 1
+        token = step[0].tolist()
+        if token[-1] in (tok.eos_id, tok.bos_id):
+            break
+        print(tok.decode(token), end="")
+        sys.stdout.flush()
+    dt = time.time() - t0
+    print(f"\n\nToken count: {count}, elapsed: {dt:.2f}s, {round(count / dt)} tokens/s")
+
+
+if __name__ == "__main__":
+    main()

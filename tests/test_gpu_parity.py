@@ -1,0 +1,211 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bar (north star): greedy token ids bit-exact; logits within 1e-4 max-abs for the
+default-scale weights; for the "sharp" weights (|logits| up to ~36) the
+reference's own test criterion, |a - b| <= 1e-4 + 2e-4 |b|
+(reference tests/test_llama_implementations.py:23-24,179).  Kernel-level
+checks compare against float64 NumPy with tolerances scaled by the sum of
+|products| (fp32 accumulation, exact-fp32 MFMA).
+"""
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import l3hip
+import llama3
+import llama3_oracle as orc
+import synth
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 1e-4, 2e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return l3hip.op_context(0)
+
+
+def _close(got, want, atol=ATOL, rtol=RTOL):
+    got = np.asarray(got, np.float64)
+    want = np.asarray(want, np.float64)
+    err = np.abs(got - want)
+    bad = err > atol + rtol * np.abs(want)
+    assert not bad.any(), f"max-abs {err.max():.3e}, worst rel {(err / (np.abs(want) + 1e-30)).max():.3e}"
+    return float(err.max())
+
+
+# ---- GEMM (MFMA fragment maps, tails, epilogues) ----------------------------------------
+
+@pytest.mark.parametrize("M,K,N", [(1, 32, 16), (16, 64, 128), (17, 288, 100), (128, 288, 288),
+                                   (200, 288, 864), (257, 768, 288), (33, 96, 1536), (4, 288, 32000)])
+def test_linear_matches_float64(ctx, M, K, N):
+    rng = np.random.default_rng(M * 7 + N)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    w = rng.standard_normal((N, K)).astype(np.float32)  # asymmetric: catches row/col swaps
+    got = ctx.op_linear(x, w)
+    want = x.astype(np.float64) @ w.astype(np.float64).T
+    scale = np.abs(x).astype(np.float64) @ np.abs(w).astype(np.float64).T
+    assert np.all(np.abs(got - want) <= 2e-6 * scale + 1e-6)
+
+
+def test_linear_integer_exact(ctx):
+    """Small integers: every product and partial sum is exact in fp32, so the MFMA path
+    must reproduce the product bit-for-bit — any fragment-map error shows up."""
+    rng = np.random.default_rng(1)
+    x = rng.integers(-4, 5, (48, 64)).astype(np.float32)
+    w = rng.integers(-4, 5, (80, 64)).astype(np.float32)
+    np.testing.assert_array_equal(ctx.op_linear(x, w), x @ w.T)
+
+
+# ---- op-level module functions vs the reference's own outputs ---------------------------
+
+def test_ops_against_golden(ctx):
+    g = load_golden("ops")
+    _close(llama3.softmax(g["softmax_x"]), g["softmax_y"], 1e-6, 1e-5)
+    _close(llama3.softmax(g["softmax_masked_x"].astype(np.float32)), g["softmax_masked_y"], 1e-6, 1e-5)
+    _close(llama3.silu(g["silu_x"]), g["silu_y"], 1e-6, 1e-5)
+    st = int(g["rope_start"])
+    q, k = llama3.apply_rotary_emb(g["rope_xq"], g["rope_xk"], g["rope_cos"][st:st + 8],
+                                   g["rope_sin"][st:st + 8])
+    _close(q, g["rope_q"], 1e-6, 1e-5)
+    _close(k, g["rope_k"], 1e-6, 1e-5)
+    _close(llama3.RMSNorm(g["rms_w"], 1e-6)(g["rms_x"]), g["rms_y"], 1e-6, 1e-5)
+    ff = llama3.FeedForward(g["ffn_wu"], g["ffn_wg"], g["ffn_wd"])
+    _close(ff(g["ffn_x"]), g["ffn_y"], 1e-5, 1e-4)
+    np.testing.assert_array_equal(llama3.repeat_kv(g["repkv_x"], 3), g["repkv_y"])
+
+
+# ---- model-level -------------------------------------------------------------------------
+
+def _model(tmp, args, hidden, seed, preset):
+    w = synth.make_weights(args, hidden, seed=seed, preset=preset)
+    path = os.path.join(tmp, f"w_{seed}_{preset}.npz")
+    synth.save_npz(path, w)
+    return w, path
+
+
+@pytest.fixture(scope="module")
+def tmpdir_mod():
+    with tempfile.TemporaryDirectory() as d:
+        yield d
+
+
+def test_tiny_sequence_against_golden(tmpdir_mod):
+    """prefill, chunked prefill at start_pos=12 (zero-prefix mask), decode — on one model."""
+    g = load_golden("tiny")
+    args = synth.tiny(4)
+    w, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, int(g["seed"]), str(g["preset"]))
+    assert synth.digest(w) == str(g["weights_sha256"])
+    m = llama3.Llama(path, args)
+    for tag in ("prefill", "chunk", "decode"):
+        out = m(g[f"{tag}_ids"], int(g[f"{tag}_start"]))
+        assert out.shape == g[f"{tag}_logits"].shape
+        _close(out, g[f"{tag}_logits"])
+
+
+def test_tiny_greedy_against_golden(tmpdir_mod):
+    g = load_golden("tiny")
+    args = synth.tiny(4)
+    _, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, int(g["seed"]), str(g["preset"]))
+    m = llama3.Llama(path, args)
+    ids = np.concatenate(list(m.generate(g["gen_prompt"], int(g["gen_max_new"]))), axis=1)
+    assert ids.dtype == np.int64
+    np.testing.assert_array_equal(ids, g["gen_ids"])
+
+
+@pytest.mark.parametrize("preset", ["default", "sharp"])
+def test_stories15m_prefill_against_golden(tmpdir_mod, preset):
+    g = load_golden(f"stories15m_{preset}")
+    args = synth.stories15m(2)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, int(g["seed"]), preset)
+    m = llama3.Llama(path, args)
+    out = m(g["prefill_ids"], 0)
+    err = _close(out, g["prefill_logits"])
+    if preset == "default":
+        assert err <= 1e-4  # north star: 1e-4 fp32 max-abs
+
+
+@pytest.mark.parametrize("preset", ["default", "sharp"])
+def test_stories15m_greedy_dream_exact(tmpdir_mod, preset):
+    """'I have a dream' -> 145 greedy steps, ids bit-exact vs the reference (decode hole included)."""
+    g = load_golden(f"stories15m_{preset}")
+    args = synth.stories15m(1)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, int(g["seed"]), preset)
+    m = llama3.Llama(path, args)
+    ids = np.concatenate(list(m.generate(g["dream_prompt"], int(g["dream_max_new"]))), axis=1)
+    np.testing.assert_array_equal(ids, g["dream_ids"])
+
+
+def test_stories15m_live_oracle_gqa_batch(tmpdir_mod):
+    """Live oracle at a size not in the fixtures: B=3, L=80 prefill then a 7-token chunk."""
+    args = synth.stories15m(3)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, args.vocab_size, (3, 80))
+    b = rng.integers(0, args.vocab_size, (3, 7))
+    assert _close(m(a, 0), ref(a, 0)) <= 1e-4
+    assert _close(m(b, 80), ref(b, 80)) <= 1e-4
+
+
+def test_transformer_block_and_attention_standalone():
+    g_args = synth.tiny(2)
+    w = synth.make_weights(g_args, synth.TINY_HIDDEN, seed=3, preset="sharp")
+    rng = np.random.default_rng(4)
+    x = rng.standard_normal((2, 10, g_args.dim)).astype(np.float32)
+    blk = llama3.TransformerBlock(w, 1, g_args)
+    ref = orc.OracleLayer(w, 1, g_args)
+    cos, sin = orc.rope_tables(g_args.dim // g_args.n_heads, g_args.max_seq_len)
+    mask = orc.causal_mask(10, 0)
+    _close(blk(x, 0, mask, cos[:10], sin[:10]), ref(x, 0, mask, cos[:10], sin[:10]))
+    # attention alone (reference Attention.__call__ on an already-normalised input)
+    xn = orc.rmsnorm(x, w["model.layers.1.input_layernorm.weight"], g_args.norm_eps)
+    p = "model.layers.1.self_attn."
+    att = llama3.Attention(w[p + "q_proj.weight"], w[p + "k_proj.weight"], w[p + "v_proj.weight"],
+                           w[p + "o_proj.weight"], g_args)
+    ref2 = orc.OracleLayer(w, 1, g_args)
+    _close(att(xn, 0, mask, cos[:10], sin[:10]), ref2.attention(xn, 0, mask, cos[:10], sin[:10]))
+
+
+def test_errors_match_reference_failure_modes(tmpdir_mod):
+    args = synth.tiny(2)
+    _, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, 1, "default")
+    m = llama3.Llama(path, args)
+    with pytest.raises(RuntimeError, match="max_batch_size"):
+        m(np.zeros((3, 4), np.int64), 0)
+    with pytest.raises(RuntimeError, match="max_seq_len"):
+        m(np.zeros((1, 4), np.int64), args.max_seq_len - 2)
+    with pytest.raises(RuntimeError, match="out of range"):
+        m(np.full((1, 2), args.vocab_size), 0)
+    # negative ids wrap like NumPy fancy indexing
+    neg = m(np.array([[-1, -2]]), 0)
+    m2 = llama3.Llama(path, args)
+    pos = m2(np.array([[args.vocab_size - 1, args.vocab_size - 2]]), 0)
+    np.testing.assert_array_equal(neg, pos)
+
+
+# ---- full-size properties (C3 shape, B=256 L=256) ------------------------------------------
+
+def test_full_size_batch_rows_independent_and_match_oracle(tmpdir_mod):
+    """At the benchmark shape, rows of one B=256 prefill equal the same rows run alone
+    (batch independence, which the multi-GPU sharding relies on), and a sample of rows
+    matches the oracle."""
+    args = synth.stories15m(256)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    m = llama3.Llama(path, args)
+    ids = np.random.default_rng(1).integers(0, args.vocab_size, (256, 256))
+    full = m(ids, 0)
+    assert np.isfinite(full).all()
+    ref = orc.OracleModel(w, synth.stories15m(1))
+    for r in (0, 131, 255):
+        m1 = llama3.Llama(path, synth.stories15m(1))
+        alone = m1(ids[r:r + 1], 0)
+        np.testing.assert_allclose(full[r:r + 1], alone, rtol=0, atol=1e-6)
+        ref = orc.OracleModel(w, synth.stories15m(1))
+        assert _close(full[r:r + 1], ref(ids[r:r + 1], 0)) <= 1e-4

@@ -1,0 +1,26 @@
+#!/bin/bash
+# Run GPU steps in order; each under its own time limit.  Exit status 0 (pass) or 1
+# (assertion / test failures) lets the next step run; anything else (fault, abort,
+# segfault, timeout) ends the call so nothing more touches the GPU.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {
+  local name=$1 limit=$2; shift 2
+  echo "=== [$name] $(date +%T) limit ${limit}s: $*"
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== [$name] rc=$rc"
+  tail -n 40 "gpurun_out/$name.log"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "fatal rc=$rc: stopping"; exit "$rc"; fi
+}
+for s in "$@"; do
+  case "$s" in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 1200 python -m pytest tests -m gpu -q -rf --timeout 600 ;;
+    testsx) step tests 1200 python -m pytest tests -m gpu -q -x -rf --timeout 600 ;;
+    bench) step bench 600 python bench.py ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
