@@ -115,8 +115,8 @@ def traffic_per_launch():
         return None
     with open(p) as f:
         d = json.load(f)
-    if d.get("workload_rows") != B_PER_GPU * SEQ:
-        return None
+    if d.get("workload_rows") != B_PER_GPU * SEQ or d.get("lib_version") != l3hip.version():
+        return None  # counters were measured on another build of the kernel
     return d.get("hbm_bytes_per_launch")
 
 

@@ -113,6 +113,13 @@ def ptr(a: np.ndarray) -> int:
     return a.ctypes.data
 
 
+def version() -> str:
+    """Library version; bumped whenever a hot kernel changes (keys profile artifacts)."""
+    major, minor = ctypes.c_int32(0), ctypes.c_int32(0)
+    check(lib().l3_version(ctypes.byref(major), ctypes.byref(minor)))
+    return f"{major.value}.{minor.value}"
+
+
 def device_count() -> int:
     n = ctypes.c_int32(0)
     check(lib().l3_device_count(ctypes.byref(n)))

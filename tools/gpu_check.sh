@@ -21,6 +21,8 @@ for s in "$@"; do
     testsx) step tests 1200 python -m pytest tests -m gpu -q -x -rf --timeout 600 ;;
     bench) step bench 600 python bench.py ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
+         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -1,0 +1,60 @@
+"""HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/pmc_gateup.json
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports exactly half of the
+bytes of a wide coalesced streaming read (TCC_EA0_RDREQ x 64 B for 128-B requests), so reads
+are doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Both counters are in KiB.
+Writes one JSON with the per-launch HBM bytes of every kernel and the headline entry for
+the fused gate|up GEMM, which bench.py reports as roofline.traffic.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+ROWS = 65536
+D, FD = 288, 768
+
+
+def load(d, counter):
+    per = defaultdict(list)
+    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if r["Counter_Name"] == counter:
+                    per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    fetch_dir, write_dir, out = sys.argv[1:4]
+    fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
+    kernels = {}
+    for k in fe:
+        f_kib = sum(fe[k]) / len(fe[k])
+        w_kib = sum(wr.get(k, [0])) / max(1, len(wr.get(k, [0])))
+        kernels[k] = {"launches": len(fe[k]), "fetch_kib_raw": round(f_kib, 1),
+                      "write_kib": round(w_kib, 1),
+                      "hbm_bytes_per_launch": int((2 * f_kib + w_kib) * 1024)}
+    gu = [k for k in kernels if "gemm_nt_kernel<2, 2, 4, 4, 2>" in k]
+    algo = 4 * (ROWS * D + 2 * FD * D + ROWS * FD)
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
+                     "python bench.py --steps 2 --warmup 1",
+           "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
+           "workload_rows": ROWS,
+           "gateup_kernel": gu[0] if gu else None,
+           "hbm_bytes_per_launch": kernels[gu[0]]["hbm_bytes_per_launch"] if gu else None,
+           "algorithmic_bytes_per_launch": algo,
+           "kernels": kernels}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+    for k, v in kernels.items():
+        print(f"{v['hbm_bytes_per_launch'] / 1e6:10.1f} MB  {k[:90]}")
+
+
+if __name__ == "__main__":
+    main()
