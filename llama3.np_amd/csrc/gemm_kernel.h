@@ -1,0 +1,346 @@
+// fp32 MFMA GEMM kernels for gfx950:  C[M,N] = A[M,K] * W[N,K]^T  with fused epilogues.
+//
+// Replaces every dense contraction of the reference forward:
+//   QKV projections      llama3.py:166-168  (+ RMSNorm :248/:111-114 fused, + RoPE :181,
+//                                            + KV-cache append :184-185)  -> EPI_QKV
+//   O projection         llama3.py:211      (+ residual :253)             -> EPI_RESID
+//   gate/up projections  llama3.py:99-101   (+ RMSNorm :256, SwiGLU)      -> EPI_SWIGLU
+//   down projection      llama3.py:102      (+ residual :259)             -> EPI_RESID
+//   lm_head              llama3.py:304-307  (+ final RMSNorm, last row)   -> EPI_STORE
+//
+// Matrix core: v_mfma_f32_16x16x4_f32 (exact fp32 in / fp32 accumulate, 64 FLOP/clk/SIMD,
+// 157.3 TF/s chip peak).  Fragment maps (cdna_hip_programming.md section 3):
+//   A: lane l supplies A[i = l&15][k = l>>4];  B: lane l supplies B[k = l>>4][j = l&15];
+//   C/D: lane l holds C[row = 4*(l>>4) + r][col = l&15], r = 0..3.
+// K-permutation trick: a sum over k may visit k in any order as long as A and B agree, so at
+// sub-step s lane l feeds k = G*(l>>4) + s for a group of 4G k values (G = 4 or 8).  One
+// 16-byte read of a K-contiguous row then yields the operands of four consecutive MFMAs, for
+// A and for W alike (both are stored K-contiguous: W is the reference's [out, in]).
+//
+// Main loop: K staged 32 deep through a double-buffered LDS image (row stride 40 floats == 8
+// mod 16: conflict-free ds_read_b128), register prefetch one tile ahead, one barrier per tile;
+// 80 KB of LDS so two blocks share a CU (measured: 1 block/CU -23%).  Rejected after
+// measurement (tools/gemm_tune): an LDS-free variant streaming fragment-shaped
+// loads straight to VGPRs (-35%) and a persistent flattened (tile, k) pipeline (-7%).
+//
+// Epilogue: values are finished in registers (RMSNorm row factor, SwiGLU), staged
+// through the now idle LDS as a row-major tile, and written back as full rows with 16-byte
+// stores (RoPE is applied there, on float4s holding whole pairs); the residual tile of
+// EPI_RESID is fetched into registers during the last k-tile so its latency hides behind the
+// MFMAs.  (Row-per-lane 4-byte stores cost 18k-50k cycles
+// per block in-kernel-stamped diagnostics — up to 60% of the main loop.)
+//
+// RMSNorm fusion: rmsnorm(x) @ W^T = diag(1/rms(x)) * (x * w_norm) @ W^T.  The norm weight
+// multiplies the A values in registers, the per-row sum of squares is accumulated from the same
+// registers, and 1/rms scales the rows in the epilogue — the normalised activations are never
+// written to HBM and W stays as stored.
+#pragma once
+#include "kernels.h"
+
+namespace l3 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float silu_f(float x) { return x * (1.0f / (1.0f + __expf(-x))); }
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// XCD-aware bijective remap of the block id: blocks b and b+8 share an XCD (L2); each XCD
+// gets a contiguous run of tile ids, so the tiles that re-read one A row panel share its L2.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+    const int xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+}
+
+// Output tile geometry of the staged epilogue.
+template <int BM, int BN, int EPI>
+struct OutTile {
+    static constexpr int COLS = EPI == EPI_SWIGLU ? BN / 2 : BN;  // output columns of the tile
+    static constexpr int STRIDE = COLS + 4;  // == 4 mod 8: the two row groups of a wave's
+                                             // ds_write_b32 land on disjoint banks
+    static constexpr int F4 = BM * COLS / 4;
+    static constexpr int IT = (F4 + 255) / 256;
+};
+
+// Phase 1+2: finish the wave's TM x TN accumulator tiles in registers and stage them,
+// row-major, into stage[BM][STRIDE].  rloc/cloc: the wave tile's first row/col in the block
+// tile; scale(i, r): RMSNorm factor of local row rloc + 16i + 4(lane>>4) + r.
+template <int BM, int BN, int TM, int TN, int EPI, typename Scale>
+__device__ __forceinline__ void stage_tile(const GemmArgs& p, f32x4 (&acc)[TM][TN], float* stage,
+                                           int m0, int n0, int rloc, int cloc, int lane,
+                                           Scale scale) {
+    using O = OutTile<BM, BN, EPI>;
+    const int frow = lane & 15, fq4 = 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int lrow = rloc + i * 16 + fq4 + r;
+            const float sc = scale(i, r);
+            float* srow = stage + lrow * O::STRIDE;
+            if constexpr (EPI == EPI_SWIGLU) {
+#pragma unroll
+                for (int j = 0; j < TN; j += 2)
+                    srow[(cloc + j * 16) / 2 + frow] = silu_f(acc[i][j][r] * sc) * (acc[i][j + 1][r] * sc);
+            } else {
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    srow[cloc + j * 16 + frow] = EPI == EPI_RESID ? acc[i][j][r] : acc[i][j][r] * sc;
+            }
+        }
+    }
+}
+
+// Residual prefetch for EPI_RESID: the same row-major float4 map phase 3 uses.
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void load_residual(const GemmArgs& p, f32x4 (&res)[OutTile<BM, BN, EPI>::IT],
+                                              int m0, int n0, int tid) {
+    using O = OutTile<BM, BN, EPI>;
+#pragma unroll
+    for (int i = 0; i < O::IT; ++i) {
+        const int f = tid + 256 * i;
+        const int lrow = f / (O::COLS / 4), col = n0 + (f % (O::COLS / 4)) * 4;
+        const int row = m0 + lrow;
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if ((O::F4 % 256 == 0 || f < O::F4) && row < p.M && col < p.N)
+            v = *reinterpret_cast<const f32x4*>(p.C + (int64_t)row * p.ldc + col);
+        res[i] = v;
+    }
+}
+
+// Phase 3: full-row 16-byte stores of the staged tile (after a barrier).  Column counts are
+// multiples of 4 (checked by launch_gemm), so a float4 never crosses the matrix edge or a
+// q|k|v section / head boundary.
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void store_tile(const GemmArgs& p, const float* stage,
+                                           const f32x4 (&res)[OutTile<BM, BN, EPI>::IT], int m0,
+                                           int n0, int tid) {
+    using O = OutTile<BM, BN, EPI>;
+    const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
+    const int c0 = EPI == EPI_SWIGLU ? n0 / 2 : n0;
+#pragma unroll
+    for (int i = 0; i < O::IT; ++i) {
+        const int f = tid + 256 * i;
+        if (!(O::F4 % 256 == 0 || f < O::F4)) continue;
+        const int lrow = f / (O::COLS / 4), lc = (f % (O::COLS / 4)) * 4;
+        const int row = m0 + lrow, col = c0 + lc;
+        if (row >= p.M || col >= ncols) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(stage + lrow * O::STRIDE + lc);
+        if constexpr (EPI == EPI_QKV) {
+            // RoPE here, where a float4 holds two whole (even, odd) pairs: one 8-byte cos and
+            // one 8-byte sin load per float4 (llama3.py:41-76), then q scaling / cache append
+            const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
+            const int bidx = row / p.L, pos = p.start_pos + row - bidx * p.L;
+            const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
+            const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
+            const int head = cc / p.HD, d = cc - head * p.HD;
+            if (is_q || is_k) {
+                const int t = pos * (p.HD >> 1) + (d >> 1);
+                const float2 c = *reinterpret_cast<const float2*>(p.rope_cos + t);
+                const float2 sn = *reinterpret_cast<const float2*>(p.rope_sin + t);
+                v = f32x4{v.x * c.x - v.y * sn.x, v.x * sn.x + v.y * c.x,
+                          v.z * c.y - v.w * sn.y, v.z * sn.y + v.w * c.y};
+            }
+            if (is_q) {
+                *reinterpret_cast<f32x4*>(p.q_out + (int64_t)row * qdim + col) = v * p.q_scale;
+            } else {
+                float* cache = is_k ? p.cache_k : p.cache_v;
+                *reinterpret_cast<f32x4*>(cache + (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d) = v;
+            }
+        } else {
+            if constexpr (EPI == EPI_RESID) v += res[i];
+            *reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + col) = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// LDS-staged main loop
+constexpr int LDS_BK = 32;
+constexpr int LDS_STRIDE = LDS_BK + 8;
+
+// In-kernel clock stamps for diagnostic builds (never in the product path): shader-clock
+// counter and the 100 MHz real-time counter, read together.
+__device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
+    unsigned long long t, rt;
+    asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(t), "=s"(rt)::"memory");
+    dst[0] = t;
+    dst[1] = rt;
+}
+
+template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false>
+__global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
+    constexpr int BM = WM * TM * 16;
+    constexpr int BN = WN * TN * 16;
+    constexpr int BK = LDS_BK;
+    constexpr int A_F4 = BM * BK / 4;
+    constexpr int B_F4 = BN * BK / 4;
+    constexpr int A_IT = (A_F4 + 255) / 256;
+    constexpr int B_IT = (B_F4 + 255) / 256;
+
+    // one LDS array: [2][BM][stride] A image, then [2][BN][stride] B image; after the main
+    // loop its head is reused for the per-row RMSNorm factors
+    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDS_STRIDE];
+    float (*As)[BM][LDS_STRIDE] = reinterpret_cast<float (*)[BM][LDS_STRIDE]>(smem);
+    float (*Bs)[BN][LDS_STRIDE] = reinterpret_cast<float (*)[BN][LDS_STRIDE]>(smem + 2 * BM * LDS_STRIDE);
+    float* row_scale = smem;
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WN, wn = wid % WN;
+    const int ntn = (p.N + BN - 1) / BN;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+    unsigned long long stamps[6];
+    if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        stamp_pair(stamps);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+
+    f32x4 ra[A_IT], rb[B_IT];
+    float ss[A_IT];
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) ss[i] = 0.f;
+
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+            const int f = tid + 256 * i;
+            const int row = f >> 3, c = (f & 7) * 4;
+            const int gm = m0 + row;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((A_F4 % 256 == 0 || f < A_F4) && gm < p.M)
+                v = *reinterpret_cast<const f32x4*>(p.A + (int64_t)gm * p.lda + k0 + c);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i) {
+            const int f = tid + 256 * i;
+            const int row = f >> 3, c = (f & 7) * 4;
+            const int gn = n0 + row;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((B_F4 % 256 == 0 || f < B_F4) && gn < p.N)
+                v = *reinterpret_cast<const f32x4*>(p.W + (int64_t)gn * p.K + k0 + c);
+            rb[i] = v;
+        }
+    };
+    auto sstore = [&](int buf, int k0) {
+        f32x4 wv = {1.f, 1.f, 1.f, 1.f};
+        if (p.norm) wv = *reinterpret_cast<const f32x4*>(p.norm_w + k0 + (tid & 7) * 4);
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+            const int f = tid + 256 * i;  // (f & 7) == (tid & 7): one norm-weight quad per thread
+            if (A_F4 % 256 == 0 || f < A_F4) {
+                f32x4 v = ra[i];
+                if (p.norm) {
+                    ss[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+                    v *= wv;
+                }
+                *reinterpret_cast<f32x4*>(&As[buf][f >> 3][(f & 7) * 4]) = v;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i) {
+            const int f = tid + 256 * i;
+            if (B_F4 % 256 == 0 || f < B_F4)
+                *reinterpret_cast<f32x4*>(&Bs[buf][f >> 3][(f & 7) * 4]) = rb[i];
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int frow = lane & 15, fk = 4 * (lane >> 4);
+    const int arow0 = wm * TM * 16, brow0 = wn * TN * 16;
+
+    auto compute = [&](int buf) {
+#pragma unroll
+        for (int kg = 0; kg < BK / 16; ++kg) {
+            f32x4 a[TM], bw[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = *reinterpret_cast<const f32x4*>(&As[buf][arow0 + i * 16 + frow][kg * 16 + fk]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bw[j] = *reinterpret_cast<const f32x4*>(&Bs[buf][brow0 + j * 16 + frow][kg * 16 + fk]);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma4(a[i][s], bw[j][s], acc[i][j]);
+        }
+    };
+
+    static_assert(((BM + 3) & ~3) + BM * OutTile<BM, BN, EPI>::STRIDE <= 2 * (BM + BN) * LDS_STRIDE,
+                  "staged output tile does not fit the LDS array");
+    f32x4 res[OutTile<BM, BN, EPI>::IT];
+
+    const int nk = p.K / BK;
+    gload(0);
+    sstore(0, 0);
+    __syncthreads();
+    for (int kt = 0; kt < nk - 1; ++kt) {
+        const int cur = kt & 1;
+        gload((kt + 1) * BK);
+        compute(cur);
+        sstore(cur ^ 1, (kt + 1) * BK);
+        __syncthreads();
+    }
+    // last k-tile, peeled: its staging registers are dead, so the residual tile of EPI_RESID is
+    // fetched here and its latency hides behind this tile's MFMAs
+    if constexpr (EPI == EPI_RESID) load_residual<BM, BN, EPI>(p, res, m0, n0, tid);
+    compute((nk - 1) & 1);
+    __syncthreads();
+
+    if (p.norm) {
+        const float inv_k = 1.0f / (float)p.K;
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+            float v = ss[i];
+            v += __shfl_xor(v, 1);
+            v += __shfl_xor(v, 2);
+            v += __shfl_xor(v, 4);
+            const int f = tid + 256 * i;
+            if ((tid & 7) == 0 && (A_F4 % 256 == 0 || f < A_F4))
+                row_scale[f >> 3] = 1.0f / sqrtf(v * inv_k + p.eps);
+        }
+        __syncthreads();
+    }
+    const bool nrm = p.norm;
+    if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        stamp_pair(stamps + 2);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // staged epilogue: the tile goes after the row factors in the (idle) LDS array
+    float* stage = smem + ((BM + 3) & ~3);
+    float sc_reg[TM][4];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc_reg[i][r] = nrm ? row_scale[arow0 + i * 16 + fk + r] : 1.0f;
+    stage_tile<BM, BN, TM, TN, EPI>(p, acc, stage, m0, n0, arow0, brow0, lane,
+                                    [&](int i, int r) { return sc_reg[i][r]; });
+    __syncthreads();
+    store_tile<BM, BN, EPI>(p, stage, res, m0, n0, tid);
+    if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        stamp_pair(stamps + 4);
+        if (tid == 0) {
+            unsigned long long* d = p.stamps + (size_t)blockIdx.x * 8;
+            for (int i = 0; i < 6; ++i) d[i] = stamps[i];
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            d[6] = xcc;
+            d[7] = t;
+        }
+    }
+}
+
+}  // namespace l3

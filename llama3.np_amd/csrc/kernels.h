@@ -27,6 +27,7 @@ struct GemmArgs {
     const float* rope_cos; const float* rope_sin;  // [Smax, HD/2]
     int L, start_pos, H, KVH, HD, Smax;
     float q_scale;
+    unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 8 per block
 };
 
 struct AttnArgs {

@@ -1,0 +1,205 @@
+// GEMM variant tuner: times kernel configurations on the stories15M prefill shapes,
+// interleaved in one process (rounds x variants), and checks every variant's output against
+// the first one.  Build: make -C tools gemm_tune ; run on the GPU box: tools/gemm_tune
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../llama3.np_amd/csrc/gemm_kernel.h"
+
+using namespace l3;
+
+#define CK(x)                                                                           \
+    do {                                                                                \
+        hipError_t e = (x);                                                             \
+        if (e != hipSuccess) {                                                          \
+            fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e), __FILE__, __LINE__); \
+            exit(2);                                                                    \
+        }                                                                               \
+    } while (0)
+
+struct Variant {
+    std::string name;
+    std::function<void(const GemmArgs&, hipStream_t)> run;
+};
+
+
+#define VAR(KERNEL, WM, WN, TM, TN, EPI, WPE)                                                       \
+    Variant{#KERNEL "<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ">", [](const GemmArgs& a, hipStream_t s) { \
+                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
+                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
+                hipLaunchKernelGGL((KERNEL<WM, WN, TM, TN, EPI, WPE, false>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
+            }}
+
+static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
+    srand(seed);
+    for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;
+}
+
+static void run_shape(const char* label, int epi, int M, int K, int N, bool norm,
+                      std::vector<Variant> vars, int rounds, int iters) {
+    const int outN = epi == EPI_SWIGLU ? N / 2 : (epi == EPI_QKV ? 288 : N);
+    std::vector<float> hA((size_t)M * K), hW((size_t)N * K), hw(K);
+    fill(hA, -1.f, 1.f, 1);
+    fill(hW, -0.05f, 0.05f, 2);
+    fill(hw, 0.5f, 1.5f, 3);
+    float *A, *W, *w, *C;
+    CK(hipMalloc(&A, hA.size() * 4));
+    CK(hipMalloc(&W, hW.size() * 4));
+    CK(hipMalloc(&w, hw.size() * 4));
+    CK(hipMalloc(&C, (size_t)M * outN * 4));
+    CK(hipMemcpy(A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(W, hW.data(), hW.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+    GemmArgs g{};
+    g.A = A; g.lda = K; g.W = W; g.C = C; g.ldc = outN; g.M = M; g.N = N; g.K = K;
+    g.norm = norm; g.norm_w = w; g.eps = 1e-6f;
+    float *qo = nullptr, *ck = nullptr, *cv = nullptr, *rc = nullptr, *rsn = nullptr;
+    if (epi == EPI_QKV) {  // stories15M attention geometry: H = KVH = 6, HD = 48, L = 256
+        g.H = 6; g.KVH = 6; g.HD = 48; g.L = 256; g.Smax = 256; g.start_pos = 0;
+        g.q_scale = 0.2f;
+        const size_t cache = (size_t)(M / 256) * 6 * 256 * 48;
+        CK(hipMalloc(&qo, (size_t)M * 288 * 4)); CK(hipMalloc(&ck, cache * 4)); CK(hipMalloc(&cv, cache * 4));
+        std::vector<float> tc(256 * 24), ts(256 * 24);
+        fill(tc, -1.f, 1.f, 4); fill(ts, -1.f, 1.f, 5);
+        CK(hipMalloc(&rc, tc.size() * 4)); CK(hipMalloc(&rsn, ts.size() * 4));
+        CK(hipMemcpy(rc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(rsn, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
+        g.q_out = qo; g.cache_k = ck; g.cache_v = cv; g.rope_cos = rc; g.rope_sin = rsn;
+        g.C = qo;  // the correctness check reads the q section
+        g.ldc = 288;
+    }
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    const double flops = 2.0 * M * N * K;
+    printf("\n== %s  M=%d K=%d N=%d epi=%d norm=%d  (%.2f GFLOP/launch)\n", label, M, K, N, epi,
+           (int)norm, flops / 1e9);
+    // correctness vs variant 0 (RESID: start from zero output each time)
+    std::vector<float> ref((size_t)M * outN), got((size_t)M * outN);
+    for (size_t v = 0; v < vars.size(); ++v) {
+        CK(hipMemsetAsync(g.C, 0, (size_t)M * outN * 4, s));
+        vars[v].run(g, s);
+        CK(hipGetLastError());
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(v ? got.data() : ref.data(), g.C, got.size() * 4, hipMemcpyDeviceToHost));
+        if (v) {
+            double md = 0, mr = 0;
+            for (size_t i = 0; i < got.size(); ++i) {
+                md = std::max(md, (double)std::fabs(got[i] - ref[i]));
+                mr = std::max(mr, (double)std::fabs(ref[i]));
+            }
+            printf("   check %-40s max|diff| %.3e (max|ref| %.3e)%s\n", vars[v].name.c_str(), md, mr,
+                   md <= 1e-4 * std::max(1.0, mr) ? "" : "  <-- MISMATCH");
+        }
+    }
+    std::vector<std::vector<double>> tf(vars.size());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int r = 0; r < rounds + 1; ++r) {
+        for (size_t v = 0; v < vars.size(); ++v) {
+            CK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i) vars[v].run(g, s);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r) tf[v].push_back(flops * iters / (ms * 1e-3) / 1e12);  // round 0 = warm-up
+        }
+    }
+    for (size_t v = 0; v < vars.size(); ++v) {
+        auto x = tf[v];
+        std::sort(x.begin(), x.end());
+        const double med = x[x.size() / 2];
+        printf("   %-44s median %7.2f TF/s (%5.1f%% of 157.3)  min %7.2f  max %7.2f  us/launch %8.1f\n",
+               vars[v].name.c_str(), med, med / 157.3 * 100, x.front(), x.back(), flops / (med * 1e12) * 1e6);
+    }
+    CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(w)); CK(hipFree(C));
+    if (qo) { CK(hipFree(qo)); CK(hipFree(ck)); CK(hipFree(cv)); CK(hipFree(rc)); CK(hipFree(rsn)); }
+    CK(hipStreamDestroy(s));
+}
+
+// Diagnostic: clock and cycle split per block from in-kernel stamps (STAMP build).
+template <int WM, int WN, int TM, int TN, int EPI>
+static void stamp_report(const char* label, int M, int K, int N, bool norm) {
+    const int outN = EPI == EPI_SWIGLU ? N / 2 : N;
+    float *A, *W, *w, *C;
+    CK(hipMalloc(&A, (size_t)M * K * 4)); CK(hipMalloc(&W, (size_t)N * K * 4));
+    CK(hipMalloc(&w, (size_t)K * 4)); CK(hipMalloc(&C, (size_t)M * outN * 4));
+    std::vector<float> hA((size_t)M * K), hW((size_t)N * K), hw(K, 1.0f);
+    fill(hA, -1.f, 1.f, 1); fill(hW, -0.05f, 0.05f, 2);
+    CK(hipMemcpy(A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(W, hW.data(), hW.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+    const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    unsigned long long* st;
+    CK(hipMalloc(&st, (size_t)tiles * 8 * 8));
+    GemmArgs g{};
+    g.A = A; g.lda = K; g.W = W; g.C = C; g.ldc = outN; g.M = M; g.N = N; g.K = K;
+    g.norm = norm; g.norm_w = w; g.eps = 1e-6f; g.stamps = st;
+    for (int it = 0; it < 20; ++it)  // >= 2 s of back-to-back launches is the guide's rule for
+        hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, 2, true>), dim3(tiles), dim3(256), 0, 0, g);
+    CK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h((size_t)tiles * 8);
+    CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> mhz, loop, epi;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int b = 0; b < tiles; ++b) {
+        const unsigned long long* d = &h[(size_t)b * 8];
+        if (d[3] > d[1]) mhz.push_back((double)(d[4] - d[0]) / (double)(d[5] - d[1]) * 100.0);
+        loop.push_back((double)(d[2] - d[0]));
+        epi.push_back((double)(d[4] - d[2]));
+        t0 = std::min(t0, d[1]); t1 = std::max(t1, d[5]);
+    }
+    auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+    const double mfma_cycles = (double)K / 4 * TM * TN * 32;  // per wave, 16x16x4 f32 at 32 cyc
+    printf("\n== stamps %s: blocks %d, clock median %.0f MHz, main loop median %.0f cyc (MFMA-only "
+           "%.0f cyc per wave), epilogue median %.0f cyc, last launch span %.1f us\n",
+           label, tiles, med(mhz), med(loop), mfma_cycles, med(epi), (t1 - t0) / 100.0);
+    CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(w)); CK(hipFree(C)); CK(hipFree(st));
+}
+
+int main(int argc, char** argv) {
+    if (argc > 3 && std::string(argv[3]) == "stamps") {
+        stamp_report<2, 2, 4, 4, EPI_SWIGLU>("gate|up 128x128", 65536, 288, 1536, true);
+        stamp_report<2, 2, 4, 3, EPI_RESID>("down 128x96", 65536, 768, 288, false);
+        stamp_report<2, 2, 4, 3, EPI_RESID>("O-proj 128x96", 65536, 288, 288, false);
+        return 0;
+    }
+    const int rounds = argc > 1 ? atoi(argv[1]) : 5;
+    const int iters = argc > 2 ? atoi(argv[2]) : 10;
+    const int M = 65536;
+    run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
+              {VAR(gemm_lds_kernel, 2, 2, 4, 4, EPI_SWIGLU, 2),
+               VAR(gemm_lds_kernel, 4, 1, 2, 8, EPI_SWIGLU, 2),
+               VAR(gemm_lds_kernel, 2, 2, 2, 4, EPI_SWIGLU, 2)},
+              rounds, iters);
+    run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+              {VAR(gemm_lds_kernel, 2, 2, 4, 3, EPI_QKV, 2),
+               VAR(gemm_lds_kernel, 4, 1, 2, 6, EPI_QKV, 2),
+               VAR(gemm_lds_kernel, 2, 2, 2, 3, EPI_QKV, 2)},
+              rounds, iters);
+    run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
+              {VAR(gemm_lds_kernel, 2, 2, 4, 3, EPI_RESID, 2),
+               VAR(gemm_lds_kernel, 2, 2, 2, 3, EPI_RESID, 2),
+               VAR(gemm_lds_kernel, 4, 1, 2, 6, EPI_RESID, 2)},
+              rounds, iters);
+    run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
+              {VAR(gemm_lds_kernel, 2, 2, 4, 3, EPI_RESID, 2),
+               VAR(gemm_lds_kernel, 2, 2, 2, 3, EPI_RESID, 2),
+               VAR(gemm_lds_kernel, 4, 1, 2, 6, EPI_RESID, 2)},
+              rounds, iters);
+    run_shape("lm_head (B=256 rows)", EPI_STORE, 256, 288, 32000, true,
+              {VAR(gemm_lds_kernel, 2, 2, 4, 4, EPI_STORE, 2),
+               VAR(gemm_lds_kernel, 2, 2, 2, 4, EPI_STORE, 2),
+               VAR(gemm_lds_kernel, 1, 4, 4, 2, EPI_STORE, 2)},
+              rounds, iters);
+    return 0;
+}

@@ -23,6 +23,9 @@ for s in "$@"; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    tune) step tune 600 tools/gemm_tune 5 10 ;;
+    stamps) step stamps 300 tools/gemm_tune 1 1 stamps ;;
+    attntune) step attntune 600 tools/attn_tune ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
