@@ -1,207 +1,13 @@
-// Fused causal attention for gfx950, fp32 MFMA (v_mfma_f32_16x16x4_f32), online softmax.
-//
-// Replaces llama3.py:186-210 — cache read (:186-187), repeat_kv (:190-191, here an index map
-// h -> h / n_rep), scores q.k^T/sqrt(HD) (:200-202), causal mask (:204-205, built at :293-297),
-// softmax (:206, :22-24), P.V (:207) and the head merge (:210).  The [B,H,L,S] score tensor
-// is never materialised.
-//
-// Orientation ("q on the lane"): every tile is computed transposed so that the query index
-// sits on lane&15 in all accumulators:
-//   S^T[key][q] = sum_d K[key][d] * Q[q][d]      (A = K tile from LDS, B = Q from registers)
-//   O^T[d][q]  += sum_key V[key][d] * P[q][key]  (A = V tile from LDS, B = P straight from the
-//                                                 S^T accumulator: lane l holds
-//                                                 P[q = l&15][key = 4(l>>4)+r], which is the
-//                                                 B operand of sub-step s = r under the
-//                                                 K-permutation trick, see gemm.hip)
-// so the running max / sum and the O rescale are lane-local, and the row max needs only two
-// cross-lane steps (xor 16, xor 32).  q is pre-scaled by log2(e)/sqrt(HD) in the QKV epilogue,
-// so p = exp2(s - m).
-//
-// Work split: a workgroup (4 waves) owns 64*QBW queries of one (batch, head); its 4*QBW
-// 16-query blocks are dealt to waves zig-zag (w, 7-w, 8+w, 15-w) so causal work is balanced.
-// K/V tiles of 64 keys are staged through double-buffered LDS (K rows padded to HD+8 floats:
-// conflict-free ds_read_b128).  Tiles / 16-key groups past a block's last query are skipped.
-#include "kernels.h"
+// Fused causal attention dispatch (kernel template and design notes: attn_kernel.h).
+#include "attn_kernel.h"
 
 namespace l3 {
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int KT = 64;  // keys per LDS tile
-
-template <int HD, int QBW>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
-    constexpr int ND = HD / 16;               // 16-wide d groups
-    constexpr int KSTR = HD + 8;              // == 8 mod 16 floats
-    constexpr int VSTR = (HD % 32 == 0) ? HD + 16 : HD;  // ds_read_b32 halves on distinct banks
-    constexpr int QW = 64 * QBW;              // queries per workgroup
-    constexpr int K_F4 = KT * HD / 4;
-    constexpr int K_IT = (K_F4 + 255) / 256;
-
-    __shared__ __attribute__((aligned(16))) float Ks[2][KT][KSTR];
-    __shared__ __attribute__((aligned(16))) float Vs[2][KT][VSTR];
-
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int kvh = h / (p.H / p.KVH);
-    const int qdim = p.H * HD;
-    const int fq = lane & 15;       // query within a 16-block
-    const int fk = 4 * (lane >> 4); // k offset of this lane's operand quad
-
-    // this wave's q blocks (zig-zag) and their last query position
-    int qblk[QBW];
-#pragma unroll
-    for (int j = 0; j < QBW; ++j) qblk[j] = (j & 1) ? (8 * (j >> 1) + 7 - wid) : (8 * (j >> 1) + wid);
-
-    // queries of this workgroup: [q_lo, q_hi) local positions
-    const int q_lo = qt * QW;
-    const int q_hi = min(p.L, q_lo + QW);
-    const int key_end = p.start_pos + q_hi;  // keys [0, key_end) are needed
-    const int ntiles = (key_end + KT - 1) / KT;
-
-    // Q fragments in registers: qreg[j][dg] = Q[q][dg*16 + fk .. +3]
-    f32x4 qreg[QBW][ND];
-    f32x4 o[QBW][ND];
-    float m_run[QBW], l_run[QBW];
-#pragma unroll
-    for (int j = 0; j < QBW; ++j) {
-        const int ql = q_lo + qblk[j] * 16 + fq;
-        const float* src = p.q + ((int64_t)b * p.L + ql) * qdim + h * HD + fk;
-#pragma unroll
-        for (int dg = 0; dg < ND; ++dg) {
-            qreg[j][dg] = (ql < p.L) ? *reinterpret_cast<const f32x4*>(src + dg * 16)
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
-            o[j][dg] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        m_run[j] = -INFINITY;
-        l_run[j] = 0.f;
-    }
-
-    const int64_t kv_base = ((int64_t)b * p.KVH + kvh) * p.Smax;
-    f32x4 rk[K_IT], rv[K_IT];
-    auto gload = [&](int tile) {
-#pragma unroll
-        for (int i = 0; i < K_IT; ++i) {
-            const int f = tid + 256 * i;
-            const int row = f / (HD / 4), c = (f % (HD / 4)) * 4;
-            const int key = tile * KT + row;
-            f32x4 vk = {0.f, 0.f, 0.f, 0.f}, vv = vk;
-            if ((K_F4 % 256 == 0 || f < K_F4) && key < p.Smax) {
-                vk = *reinterpret_cast<const f32x4*>(p.cache_k + (kv_base + key) * HD + c);
-                vv = *reinterpret_cast<const f32x4*>(p.cache_v + (kv_base + key) * HD + c);
-            }
-            rk[i] = vk;
-            rv[i] = vv;
-        }
-    };
-    auto sstore = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < K_IT; ++i) {
-            const int f = tid + 256 * i;
-            if (K_F4 % 256 == 0 || f < K_F4) {
-                const int row = f / (HD / 4), c = (f % (HD / 4)) * 4;
-                *reinterpret_cast<f32x4*>(&Ks[buf][row][c]) = rk[i];
-                *reinterpret_cast<f32x4*>(&Vs[buf][row][c]) = rv[i];
-            }
-        }
-    };
-
-    gload(0);
-    sstore(0);
-    __syncthreads();
-    for (int tile = 0; tile < ntiles; ++tile) {
-        const int cur = tile & 1;
-        if (tile + 1 < ntiles) gload(tile + 1);
-        const int k0 = tile * KT;
-#pragma unroll
-        for (int j = 0; j < QBW; ++j) {
-            const int qblock_first = q_lo + qblk[j] * 16;
-            if (qblock_first >= p.L) continue;                        // padding block
-            const int qmax_abs = p.start_pos + min(qblock_first + 15, p.L - 1);
-            if (k0 > qmax_abs) continue;                              // whole tile masked
-            const int q_abs = p.start_pos + qblock_first + fq;
-            f32x4 sacc[4];
-            bool live[4];
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg) {
-                live[kg] = (k0 + kg * 16) <= qmax_abs;                // wave-uniform
-                sacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if (live[kg]) {
-#pragma unroll
-                    for (int dg = 0; dg < ND; ++dg) {
-                        const f32x4 kf = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
-#pragma unroll
-                        for (int s = 0; s < 4; ++s)
-                            sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
-                    }
-                }
-            }
-            // causal mask + tile max (lane holds keys k0 + kg*16 + fk + r for query q_abs)
-            float mt = -INFINITY;
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int key = k0 + kg * 16 + fk + r;
-                    const float v = (live[kg] && key <= q_abs) ? sacc[kg][r] : -INFINITY;
-                    sacc[kg][r] = v;
-                    mt = fmaxf(mt, v);
-                }
-            mt = fmaxf(mt, __shfl_xor(mt, 16));
-            mt = fmaxf(mt, __shfl_xor(mt, 32));
-            const float m_new = fmaxf(m_run[j], mt);
-            const float alpha = exp2f(m_run[j] - m_new);   // 0 on the first tile
-            m_run[j] = m_new;
-            float psum = 0.f;
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float pv = exp2f(sacc[kg][r] - m_new);
-                    sacc[kg][r] = pv;
-                    psum += pv;
-                }
-            l_run[j] = l_run[j] * alpha + psum;
-#pragma unroll
-            for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;
-#pragma unroll
-            for (int kg = 0; kg < 4; ++kg) {
-                if (!live[kg]) continue;
-#pragma unroll
-                for (int dg = 0; dg < ND; ++dg)
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const float vf = Vs[cur][kg * 16 + fk + s][dg * 16 + fq];
-                        o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);
-                    }
-            }
-        }
-        if (tile + 1 < ntiles) sstore(cur ^ 1);
-        __syncthreads();
-    }
-
-    // finalize: l = sum over the 4 lane groups; lane holds O^T[d = dg*16 + fk + r][q = fq]
-#pragma unroll
-    for (int j = 0; j < QBW; ++j) {
-        float l = l_run[j];
-        l += __shfl_xor(l, 16);
-        l += __shfl_xor(l, 32);
-        const int ql = q_lo + qblk[j] * 16 + fq;
-        if (ql < p.L) {
-            const float inv = 1.0f / l;
-            float* dst = p.out + ((int64_t)b * p.L + ql) * qdim + h * HD + fk;
-#pragma unroll
-            for (int dg = 0; dg < ND; ++dg)
-                *reinterpret_cast<f32x4*>(dst + dg * 16) = o[j][dg] * inv;
-        }
-    }
-}
-
-template <int HD, int QBW>
+template <int HD, int QBW, bool VT = false>
 static hipError_t launch_hd(const AttnArgs& a, hipStream_t s) {
     constexpr int QW = 64 * QBW;
     dim3 grid((a.L + QW - 1) / QW, a.H, a.B), block(256);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, VT>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 

@@ -1,0 +1,107 @@
+// Attention variant tuner: times attn_fwd_kernel configurations interleaved in one process
+// and checks each against the first.  Build: make -C tools attn_tune ; run: tools/attn_tune
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../llama3.np_amd/csrc/attn_kernel.h"
+
+using namespace l3;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e = (x);                                                                   \
+        if (e != hipSuccess) {                                                                \
+            fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e), __FILE__, __LINE__); \
+            exit(2);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+struct Variant {
+    std::string name;
+    std::function<void(const AttnArgs&, hipStream_t)> run;
+};
+
+#define AVAR(HD, QBW, VT)                                                                     \
+    Variant{"attn<" #HD "," #QBW "," #VT ">", [](const AttnArgs& a, hipStream_t s) {         \
+                constexpr int QW = 64 * QBW;                                                  \
+                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
+                hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, VT>), grid, dim3(256), 0, s, a); \
+            }}
+
+static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
+    srand(seed);
+    for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;
+}
+
+static void run(const char* label, int B, int L, int H, int KVH, int HD, std::vector<Variant> vars,
+                int rounds, int iters) {
+    const int Smax = L;
+    const size_t nq = (size_t)B * L * H * HD, nkv = (size_t)B * KVH * Smax * HD;
+    std::vector<float> hq(nq), hk(nkv), hv(nkv);
+    fill(hq, -1.f, 1.f, 1);
+    fill(hk, -1.f, 1.f, 2);
+    fill(hv, -1.f, 1.f, 3);
+    float *q, *k, *v, *o;
+    CK(hipMalloc(&q, nq * 4)); CK(hipMalloc(&k, nkv * 4)); CK(hipMalloc(&v, nkv * 4)); CK(hipMalloc(&o, nq * 4));
+    CK(hipMemcpy(q, hq.data(), nq * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(k, hk.data(), nkv * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(v, hv.data(), nkv * 4, hipMemcpyHostToDevice));
+    AttnArgs a{};
+    a.q = q; a.cache_k = k; a.cache_v = v; a.out = o;
+    a.B = B; a.L = L; a.start_pos = 0; a.H = H; a.KVH = KVH; a.HD = HD; a.Smax = Smax;
+    const double flops = 4.0 * HD * H * (double)B * L * (L + 1) / 2;  // causal useful half
+    printf("\n== %s B=%d L=%d H=%d KVH=%d HD=%d (%.2f GFLOP useful)\n", label, B, L, H, KVH, HD, flops / 1e9);
+    std::vector<float> ref(nq), got(nq);
+    for (size_t i = 0; i < vars.size(); ++i) {
+        CK(hipMemset(o, 0, nq * 4));
+        vars[i].run(a, 0);
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(i ? got.data() : ref.data(), o, nq * 4, hipMemcpyDeviceToHost));
+        if (i) {
+            double md = 0;
+            for (size_t t = 0; t < nq; ++t) md = std::max(md, (double)std::fabs(got[t] - ref[t]));
+            printf("   check %-20s max|diff| %.3e%s\n", vars[i].name.c_str(), md, md < 1e-4 ? "" : "  <-- MISMATCH");
+        }
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    std::vector<std::vector<double>> tf(vars.size());
+    for (int r = 0; r <= rounds; ++r)
+        for (size_t i = 0; i < vars.size(); ++i) {
+            CK(hipEventRecord(e0, 0));
+            for (int it = 0; it < iters; ++it) vars[i].run(a, 0);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r) tf[i].push_back(flops * iters / (ms * 1e-3) / 1e12);
+        }
+    for (size_t i = 0; i < vars.size(); ++i) {
+        auto x = tf[i];
+        std::sort(x.begin(), x.end());
+        const double med = x[x.size() / 2];
+        printf("   %-22s median %7.2f TF/s (%5.1f%%)  us/launch %8.1f\n", vars[i].name.c_str(), med,
+               med / 157.3 * 100, flops / (med * 1e12) * 1e6);
+    }
+    CK(hipFree(q)); CK(hipFree(k)); CK(hipFree(v)); CK(hipFree(o));
+}
+
+int main(int argc, char** argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
+    run("stories15M C3", 256, 256, 6, 6, 48,
+        {AVAR(48, 4, false), AVAR(48, 4, true), AVAR(48, 2, false), AVAR(48, 2, true),
+         AVAR(48, 1, true)},
+        rounds, iters);
+    run("Llama-3 shape (C5 slice)", 4, 2048, 32, 8, 128,
+        {AVAR(128, 2, false), AVAR(128, 2, true), AVAR(128, 1, true), AVAR(128, 1, false)},
+        rounds, 3);
+    return 0;
+}

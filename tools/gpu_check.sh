@@ -26,6 +26,7 @@ for s in "$@"; do
     tune) step tune 600 tools/gemm_tune 5 10 ;;
     stamps) step stamps 300 tools/gemm_tune 1 1 stamps ;;
     attntune) step attntune 600 tools/attn_tune ;;
+    rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
