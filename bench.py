@@ -120,13 +120,92 @@ def traffic_per_launch():
     return d.get("hbm_bytes_per_launch")
 
 
+def bench_c5(a):
+    """BASELINE configs[4]: Llama-3-8B-shaped prefill (D 4096, 32 layers, H 32 / KVH 8,
+    FD 14336, VS 128256), B=64, L=2048 on one GPU — a roofline report, not the headline line.
+    Weights (32 GB fp32) are synthetic and uploaded tensor by tensor through the C ABI
+    (uniform with std 0.02 drawn from a 256M-float pool: an 8.5G-sample normal draw would take
+    minutes); the forward is the same l3_forward_dev as the headline bench."""
+    args = synth.llama3_shape(n_layers=a.layers, max_batch_size=64, max_seq_len=2048)
+    D, FD, VS, H, KVH = args.dim, synth.LLAMA3_HIDDEN, args.vocab_size, args.n_heads, args.kv_heads
+    HD = D // H
+    B, L = 64, 2048
+    dims = l3hip.Dims(dim=D, n_layers=args.n_layers, n_heads=H, n_kv_heads=KVH, vocab_size=VS,
+                      hidden_dim=FD, max_seq_len=L, max_batch_size=B, norm_eps=args.norm_eps)
+    ctx = l3hip.Context(dims, 0)
+    rng = np.random.default_rng(0)
+    pool = (rng.random(1 << 28, dtype=np.float32) * 2 - 1) * np.float32(0.02 * 3 ** 0.5)
+
+    def tensor(shape):
+        n = int(np.prod(shape))
+        if n <= pool.size:
+            o = int(rng.integers(0, pool.size - n + 1))
+            return pool[o:o + n].reshape(shape)
+        return np.resize(pool, n).reshape(shape)
+
+    t_up = time.perf_counter()
+    ctx.upload(0, l3hip.W_EMBED, np.resize(pool * np.float32(50.0), VS * D).reshape(VS, D))
+    for i in range(args.n_layers):
+        for kind, shape in ((l3hip.W_Q, (H * HD, D)), (l3hip.W_K, (KVH * HD, D)), (l3hip.W_V, (KVH * HD, D)),
+                            (l3hip.W_O, (D, H * HD)), (l3hip.W_GATE, (FD, D)), (l3hip.W_UP, (FD, D)),
+                            (l3hip.W_DOWN, (D, FD))):
+            ctx.upload(i, kind, tensor(shape))
+        ctx.upload(i, l3hip.W_ATTN_NORM, np.ones(D, np.float32))
+        ctx.upload(i, l3hip.W_FFN_NORM, np.ones(D, np.float32))
+    ctx.upload(0, l3hip.W_FINAL_NORM, np.ones(D, np.float32))
+    ctx.upload(0, l3hip.W_LM_HEAD, tensor((VS, D)))
+    ctx.finalize()
+    t_up = time.perf_counter() - t_up
+    ids = rng.integers(0, VS, (B, L)).astype(np.int32)
+    ids_dev = ctx.alloc(ids.nbytes)
+    ctx.h2d(ids_dev, ids)
+    logits_dev = ctx.alloc(B * VS * 4)
+    for _ in range(a.warmup):
+        ctx.forward_dev(ids_dev, B, L, 0, logits_dev)
+    ctx.synchronize()
+    ctx.kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.forward_dev(ids_dev, B, L, 0, logits_dev)
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    st = ctx.kernel_stats()
+    T = B * L
+    flops = {"qkv": 2.0 * T * D * (H + 2 * KVH) * HD, "oproj": 2.0 * T * D * D,
+             "gateup": 2.0 * T * D * 2 * FD, "down": 2.0 * T * FD * D,
+             "attn": 4.0 * HD * H * B * L * (L + 1) / 2, "lmhead": 2.0 * B * D * VS}
+    total = args.n_layers * sum(v for k, v in flops.items() if k != "lmhead") + flops["lmhead"]
+    per = {k: {"ms": round(st[k][0] / st[k][1], 3),
+               "TFLOP/s": round(flops[k] / (st[k][0] / st[k][1] / 1e3) / 1e12, 1)}
+           for k in flops if st[k][1]}
+    gu = per["gateup"]["TFLOP/s"]
+    print(json.dumps({
+        "metric": "tokens/s Llama-3-shape prefill B=64 L=2048 (roofline report, BASELINE configs[4])",
+        "value": round(T * a.steps / el, 1), "unit": "tokens/s", "n_gpus": 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 1), "higher_is_better": True,
+        "dtype": "fp32", "data": "synthetic uniform weights (std 0.02), uniform random ids",
+        "config": {"workload": f"Llama-3-8B shape, {args.n_layers} layers, B=64 L=2048",
+                   "global_batch": B, "seq_len": L},
+        "whole_forward_TFLOP/s": round(total * a.steps / el / 1e12, 1),
+        "whole_forward_frac": round(total * a.steps / el / 1e12 / PEAK_FP32_TFLOPS, 4),
+        "roofline": {"kernel": "gemm gate|up, M=131072 K=4096 N=28672", "bound": "mfma",
+                     "achieved": gu, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(gu / PEAK_FP32_TFLOPS, 4), "traffic": None},
+        "kernels": per, "weight_upload_s": round(t_up, 1)}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=["c3", "c5"], default="c3",
+                    help="c3: headline stories15M B=256 L=256 (default); c5: Llama-3-shape report")
+    ap.add_argument("--layers", type=int, default=32, help="c5 only")
     a = ap.parse_args()
+    if a.workload == "c5":
+        return bench_c5(a)
 
     dist = Dist(a.gpus)
     dev = dist.local_rank

@@ -1,0 +1,48 @@
+"""Greedy-decode benchmark (BASELINE configs[0..1]): stories15M, B=1, prompt ids of
+"I have a dream" = [1, 76, 505, 263, 12561], max_new_tokens=150 -> 145 greedy steps through
+Llama.generate (the reference's loop, llama3.py:310-321, device argmax, ids-only D2H).
+
+Prints one JSON line: tokens/s counted the reference's way (prompt + generated tokens over
+wall time including prefill, llama3.py:347-349), per-step latency, and the ids check against
+the committed golden (fixture from the reference itself).
+"""
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "llama3.np_amd"))
+import llama3  # noqa: E402
+import synth  # noqa: E402
+
+
+def main():
+    g = np.load(os.path.join(REPO, "tests", "golden", "stories15m_default.npz"))
+    args = synth.stories15m(1)
+    w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=int(g["seed"]), preset="default")
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "w.npz")
+        synth.save_npz(p, w)
+        model = llama3.Llama(p, args)
+    prompt = g["dream_prompt"]
+    list(model.generate(prompt, 20))  # warm-up (caches are overwritten by the timed run)
+    runs = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ids = [int(x[0, 0]) for x in model.generate(prompt, int(g["dream_max_new"]))]
+        runs.append(time.perf_counter() - t0)
+    exact = ids == g["dream_ids"][0].tolist()
+    t = float(np.median(runs))
+    count = prompt.shape[1] + len(ids)
+    print(json.dumps({"workload": "stories15M greedy decode B=1, 'I have a dream', 145 steps",
+                      "tokens_per_s_reference_count": round(count / t, 1),
+                      "generated_tokens_per_s": round(len(ids) / t, 1),
+                      "ms_per_step": round(t / len(ids) * 1e3, 3), "ids_exact_vs_reference": exact}))
+
+
+if __name__ == "__main__":
+    main()

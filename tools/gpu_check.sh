@@ -26,6 +26,9 @@ for s in "$@"; do
     tune) step tune 600 tools/gemm_tune 5 10 ;;
     stamps) step stamps 300 tools/gemm_tune 1 1 stamps ;;
     attntune) step attntune 600 tools/attn_tune ;;
+    decode) step decode 300 python tools/bench_decode.py ;;
+    c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
+    c5small) step c5small 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
