@@ -62,6 +62,10 @@ struct OutTile {
                                              // ds_write_b32 land on disjoint banks
     static constexpr int F4 = BM * COLS / 4;
     static constexpr int IT = (F4 + 255) / 256;
+    // EPI_RESID: prefetch the residual tile into registers during the last k-tile when it is
+    // at most 12 float4 per thread (64x96, 128x96); larger tiles (128x128, long-K shapes) load
+    // it in the store phase instead of spilling
+    static constexpr bool RES_PREFETCH = IT <= 12;
 };
 
 // Phase 1+2: finish the wave's TM x TN accumulator tiles in registers and stage them,
@@ -94,8 +98,8 @@ __device__ __forceinline__ void stage_tile(const GemmArgs& p, f32x4 (&acc)[TM][T
 }
 
 // Residual prefetch for EPI_RESID: the same row-major float4 map phase 3 uses.
-template <int BM, int BN, int EPI>
-__device__ __forceinline__ void load_residual(const GemmArgs& p, f32x4 (&res)[OutTile<BM, BN, EPI>::IT],
+template <int BM, int BN, int EPI, int NR>
+__device__ __forceinline__ void load_residual(const GemmArgs& p, f32x4 (&res)[NR],
                                               int m0, int n0, int tid) {
     using O = OutTile<BM, BN, EPI>;
 #pragma unroll
@@ -113,9 +117,9 @@ __device__ __forceinline__ void load_residual(const GemmArgs& p, f32x4 (&res)[Ou
 // Phase 3: full-row 16-byte stores of the staged tile (after a barrier).  Column counts are
 // multiples of 4 (checked by launch_gemm), so a float4 never crosses the matrix edge or a
 // q|k|v section / head boundary.
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, int NR>
 __device__ __forceinline__ void store_tile(const GemmArgs& p, const float* stage,
-                                           const f32x4 (&res)[OutTile<BM, BN, EPI>::IT], int m0,
+                                           const f32x4 (&res)[NR], int m0,
                                            int n0, int tid) {
     using O = OutTile<BM, BN, EPI>;
     const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
@@ -150,7 +154,10 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, const float* stage
                 *reinterpret_cast<f32x4*>(cache + (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d) = v;
             }
         } else {
-            if constexpr (EPI == EPI_RESID) v += res[i];
+            if constexpr (EPI == EPI_RESID) {
+                if constexpr (O::RES_PREFETCH) v += res[i];
+                else v += *reinterpret_cast<const f32x4*>(p.C + (int64_t)row * p.ldc + col);
+            }
             *reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + col) = v;
         }
     }
@@ -158,8 +165,6 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, const float* stage
 
 // ---------------------------------------------------------------------------------------
 // LDS-staged main loop
-constexpr int LDS_BK = 32;
-constexpr int LDS_STRIDE = LDS_BK + 8;
 
 // In-kernel clock stamps for diagnostic builds (never in the product path): shader-clock
 // counter and the 100 MHz real-time counter, read together.
@@ -170,19 +175,24 @@ __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
     dst[1] = rt;
 }
 
-template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false>
+template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false,
+          int BK = 32>
 __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
     constexpr int BM = WM * TM * 16;
     constexpr int BN = WN * TN * 16;
-    constexpr int BK = LDS_BK;
+    constexpr int LDS_STRIDE = BK + 8;  // == 8 mod 16 floats for BK in {16, 32, 64}
+    constexpr int Q = BK / 4;           // float4 per staged row
+    static_assert(BK % 16 == 0 && (Q & (Q - 1)) == 0, "BK must be 16, 32 or 64");
     constexpr int A_F4 = BM * BK / 4;
     constexpr int B_F4 = BN * BK / 4;
     constexpr int A_IT = (A_F4 + 255) / 256;
     constexpr int B_IT = (B_F4 + 255) / 256;
 
     // one LDS array: [2][BM][stride] A image, then [2][BN][stride] B image; after the main
-    // loop its head is reused for the per-row RMSNorm factors
-    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDS_STRIDE];
+    // loop its head holds the per-row RMSNorm factors, then the staged output tile
+    constexpr int MAIN_F = 2 * (BM + BN) * LDS_STRIDE;
+    constexpr int EPI_F = ((BM + 3) & ~3) + BM * OutTile<BM, BN, EPI>::STRIDE;
+    __shared__ __attribute__((aligned(16))) float smem[MAIN_F > EPI_F ? MAIN_F : EPI_F];
     float (*As)[BM][LDS_STRIDE] = reinterpret_cast<float (*)[BM][LDS_STRIDE]>(smem);
     float (*Bs)[BN][LDS_STRIDE] = reinterpret_cast<float (*)[BN][LDS_STRIDE]>(smem + 2 * BM * LDS_STRIDE);
     float* row_scale = smem;
@@ -208,7 +218,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 #pragma unroll
         for (int i = 0; i < A_IT; ++i) {
             const int f = tid + 256 * i;
-            const int row = f >> 3, c = (f & 7) * 4;
+            const int row = f / Q, c = (f % Q) * 4;
             const int gm = m0 + row;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if ((A_F4 % 256 == 0 || f < A_F4) && gm < p.M)
@@ -218,7 +228,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
             const int f = tid + 256 * i;
-            const int row = f >> 3, c = (f & 7) * 4;
+            const int row = f / Q, c = (f % Q) * 4;
             const int gn = n0 + row;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if ((B_F4 % 256 == 0 || f < B_F4) && gn < p.N)
@@ -228,24 +238,24 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     };
     auto sstore = [&](int buf, int k0) {
         f32x4 wv = {1.f, 1.f, 1.f, 1.f};
-        if (p.norm) wv = *reinterpret_cast<const f32x4*>(p.norm_w + k0 + (tid & 7) * 4);
+        if (p.norm) wv = *reinterpret_cast<const f32x4*>(p.norm_w + k0 + (tid % Q) * 4);
 #pragma unroll
         for (int i = 0; i < A_IT; ++i) {
-            const int f = tid + 256 * i;  // (f & 7) == (tid & 7): one norm-weight quad per thread
+            const int f = tid + 256 * i;  // f % Q == tid % Q: one norm-weight quad per thread
             if (A_F4 % 256 == 0 || f < A_F4) {
                 f32x4 v = ra[i];
                 if (p.norm) {
                     ss[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
                     v *= wv;
                 }
-                *reinterpret_cast<f32x4*>(&As[buf][f >> 3][(f & 7) * 4]) = v;
+                *reinterpret_cast<f32x4*>(&As[buf][f / Q][(f % Q) * 4]) = v;
             }
         }
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
             const int f = tid + 256 * i;
             if (B_F4 % 256 == 0 || f < B_F4)
-                *reinterpret_cast<f32x4*>(&Bs[buf][f >> 3][(f & 7) * 4]) = rb[i];
+                *reinterpret_cast<f32x4*>(&Bs[buf][f / Q][(f % Q) * 4]) = rb[i];
         }
     };
 
@@ -277,9 +287,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         }
     };
 
-    static_assert(((BM + 3) & ~3) + BM * OutTile<BM, BN, EPI>::STRIDE <= 2 * (BM + BN) * LDS_STRIDE,
-                  "staged output tile does not fit the LDS array");
-    f32x4 res[OutTile<BM, BN, EPI>::IT];
+    f32x4 res[OutTile<BM, BN, EPI>::RES_PREFETCH ? OutTile<BM, BN, EPI>::IT : 1];
 
     const int nk = p.K / BK;
     gload(0);
@@ -294,7 +302,8 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     }
     // last k-tile, peeled: its staging registers are dead, so the residual tile of EPI_RESID is
     // fetched here and its latency hides behind this tile's MFMAs
-    if constexpr (EPI == EPI_RESID) load_residual<BM, BN, EPI>(p, res, m0, n0, tid);
+    if constexpr (EPI == EPI_RESID && OutTile<BM, BN, EPI>::RES_PREFETCH)
+        load_residual<BM, BN, EPI>(p, res, m0, n0, tid);
     compute((nk - 1) & 1);
     __syncthreads();
 
@@ -303,12 +312,11 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 #pragma unroll
         for (int i = 0; i < A_IT; ++i) {
             float v = ss[i];
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            v += __shfl_xor(v, 4);
+#pragma unroll
+            for (int o = 1; o < Q; o <<= 1) v += __shfl_xor(v, o);  // the Q lanes of one row
             const int f = tid + 256 * i;
-            if ((tid & 7) == 0 && (A_F4 % 256 == 0 || f < A_F4))
-                row_scale[f >> 3] = 1.0f / sqrtf(v * inv_k + p.eps);
+            if ((tid % Q) == 0 && (A_F4 % 256 == 0 || f < A_F4))
+                row_scale[f / Q] = 1.0f / sqrtf(v * inv_k + p.eps);
         }
         __syncthreads();
     }

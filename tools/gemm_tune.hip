@@ -37,6 +37,13 @@ struct Variant {
                 hipLaunchKernelGGL((KERNEL<WM, WN, TM, TN, EPI, WPE, false>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
             }}
 
+#define BVAR(WM, WN, TM, TN, EPI, WPE, BK)                                                            \
+    Variant{"lds<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
+                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
+                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
+                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
+            }}
+
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
     for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;
@@ -176,30 +183,31 @@ int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5;
     const int iters = argc > 2 ? atoi(argv[2]) : 10;
     const int M = 65536;
+    const bool c5 = argc > 3 && std::string(argv[3]) == "c5";
+    if (!c5) {
     run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
-              {VAR(gemm_lds_kernel, 2, 2, 4, 4, EPI_SWIGLU, 2),
-               VAR(gemm_lds_kernel, 4, 1, 2, 8, EPI_SWIGLU, 2),
-               VAR(gemm_lds_kernel, 2, 2, 2, 4, EPI_SWIGLU, 2)},
-              rounds, iters);
+              {BVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 16), BVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16)}, rounds, iters);
     run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
-              {VAR(gemm_lds_kernel, 2, 2, 4, 3, EPI_QKV, 2),
-               VAR(gemm_lds_kernel, 4, 1, 2, 6, EPI_QKV, 2),
-               VAR(gemm_lds_kernel, 2, 2, 2, 3, EPI_QKV, 2)},
-              rounds, iters);
+              {BVAR(2, 2, 2, 3, EPI_QKV, 3, 16), BVAR(2, 2, 2, 3, EPI_QKV, 4, 16)}, rounds, iters);
     run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
-              {VAR(gemm_lds_kernel, 2, 2, 4, 3, EPI_RESID, 2),
-               VAR(gemm_lds_kernel, 2, 2, 2, 3, EPI_RESID, 2),
-               VAR(gemm_lds_kernel, 4, 1, 2, 6, EPI_RESID, 2)},
-              rounds, iters);
+              {BVAR(2, 2, 4, 3, EPI_RESID, 2, 32)}, rounds, iters);
     run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
-              {VAR(gemm_lds_kernel, 2, 2, 4, 3, EPI_RESID, 2),
-               VAR(gemm_lds_kernel, 2, 2, 2, 3, EPI_RESID, 2),
-               VAR(gemm_lds_kernel, 4, 1, 2, 6, EPI_RESID, 2)},
-              rounds, iters);
-    run_shape("lm_head (B=256 rows)", EPI_STORE, 256, 288, 32000, true,
-              {VAR(gemm_lds_kernel, 2, 2, 4, 4, EPI_STORE, 2),
-               VAR(gemm_lds_kernel, 2, 2, 2, 4, EPI_STORE, 2),
-               VAR(gemm_lds_kernel, 1, 4, 4, 2, EPI_STORE, 2)},
-              rounds, iters);
+              {BVAR(2, 2, 2, 3, EPI_RESID, 2, 32)}, rounds, iters);
+    } else {
+    // Llama-3-8B shapes (C5) at M = 16384 rows (tuning size)
+    const int Mc = 16384;
+    run_shape("C5 gate|up", EPI_SWIGLU, Mc, 4096, 28672, true,
+              {BVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32), BVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 16),
+               BVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16)}, rounds, 3);
+    run_shape("C5 QKV-shape (store)", EPI_STORE, Mc, 4096, 6144, true,
+              {BVAR(2, 2, 4, 3, EPI_STORE, 2, 32), BVAR(2, 2, 2, 3, EPI_STORE, 3, 16),
+               BVAR(2, 2, 4, 4, EPI_STORE, 2, 16), BVAR(2, 2, 4, 3, EPI_STORE, 3, 16)}, rounds, 3);
+    run_shape("C5 O-proj", EPI_RESID, Mc, 4096, 4096, false,
+              {BVAR(2, 2, 2, 4, EPI_RESID, 2, 32), BVAR(2, 2, 4, 4, EPI_RESID, 2, 16),
+               BVAR(2, 2, 2, 4, EPI_RESID, 3, 16), BVAR(2, 2, 4, 4, EPI_RESID, 2, 32)}, rounds, 3);
+    run_shape("C5 down", EPI_RESID, Mc, 14336, 4096, false,
+              {BVAR(2, 2, 2, 4, EPI_RESID, 2, 32), BVAR(2, 2, 4, 4, EPI_RESID, 2, 16),
+               BVAR(2, 2, 2, 4, EPI_RESID, 3, 16)}, rounds, 3);
+    }
     return 0;
 }

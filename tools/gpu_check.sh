@@ -24,6 +24,7 @@ for s in "$@"; do
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     tune) step tune 600 tools/gemm_tune 5 10 ;;
+    tunec5) step tunec5 900 tools/gemm_tune 3 3 c5 ;;
     stamps) step stamps 300 tools/gemm_tune 1 1 stamps ;;
     attntune) step attntune 600 tools/attn_tune ;;
     decode) step decode 300 python tools/bench_decode.py ;;
