@@ -3,24 +3,40 @@
 
 namespace l3 {
 
-template <int HD, int QBW, bool VT = false>
-static hipError_t launch_hd(const AttnArgs& a, hipStream_t s) {
-    constexpr int QW = 64 * QBW;
-    dim3 grid((a.L + QW - 1) / QW, a.H, a.B), block(256);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, VT>), grid, block, 0, s, a);
+template <int HD, int QBW, int G, int KT>
+static hipError_t launch(const AttnArgs& a, hipStream_t s) {
+    constexpr int QW = 16 * QBW * (4 / G);
+    dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B), block(256);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, block, 0, s, a);
     return hipGetLastError();
+}
+
+// G = heads per workgroup sharing one KV head; QBW = 16-query blocks per wave (chosen so a
+// workgroup's query range does not far exceed L; QBIG for long prompts, tools/attn_tune).
+template <int HD, int KT, int QBIG, int G>
+static hipError_t launch_g(const AttnArgs& a, hipStream_t s) {
+    constexpr int WPH = 4 / G;
+    if (a.L <= 16 * WPH) return launch<HD, 1, G, KT>(a, s);
+    if (QBIG > 2 && a.L <= 32 * WPH) return launch<HD, 2, G, KT>(a, s);
+    return launch<HD, QBIG, G, KT>(a, s);
+}
+
+template <int HD, int KT, int QBIG>
+static hipError_t launch_hd(const AttnArgs& a, hipStream_t s) {
+    const int n_rep = a.H / a.KVH;
+    if (n_rep % 4 == 0) return launch_g<HD, KT, QBIG, 4>(a, s);
+    if (n_rep % 2 == 0) return launch_g<HD, KT, QBIG, 2>(a, s);
+    return launch_g<HD, KT, QBIG, 1>(a, s);
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (a.B <= 0 || a.L <= 0) return hipSuccess;
-    if (a.H % a.KVH != 0) return hipErrorInvalidValue;
-    // small L (decode, short prompts): one 16-query block per wave is enough
-    const bool small = a.L <= 64;
+    if (a.KVH <= 0 || a.H % a.KVH != 0) return hipErrorInvalidValue;
     switch (a.HD) {
-        case 16: return small ? launch_hd<16, 1>(a, s) : launch_hd<16, 4>(a, s);
-        case 48: return small ? launch_hd<48, 1>(a, s) : launch_hd<48, 4>(a, s);
-        case 64: return small ? launch_hd<64, 1>(a, s) : launch_hd<64, 2>(a, s);
-        case 128: return small ? launch_hd<128, 1>(a, s) : launch_hd<128, 2>(a, s);
+        case 16: return launch_hd<16, 64, 4>(a, s);
+        case 48: return launch_hd<48, 64, 4>(a, s);
+        case 64: return launch_hd<64, 64, 4>(a, s);
+        case 128: return launch_hd<128, 32, 2>(a, s);  // KT 32: 72 KB LDS -> 2 workgroups per CU
         default: return hipErrorInvalidValue;
     }
 }

@@ -12,14 +12,16 @@
 //                                                 S^T accumulator: lane l holds
 //                                                 P[q = l&15][key = 4(l>>4)+r], which is the
 //                                                 B operand of sub-step s = r under the
-//                                                 K-permutation trick, see gemm.hip)
+//                                                 K-permutation trick, see gemm_kernel.h)
 // so the running max / sum and the O rescale are lane-local, and the row max needs only two
 // cross-lane steps (xor 16, xor 32).  q is pre-scaled by log2(e)/sqrt(HD) in the QKV epilogue,
 // so p = exp2(s - m).
 //
-// Work split: a workgroup (4 waves) owns 64*QBW queries of one (batch, head); its 4*QBW
-// 16-query blocks are dealt to waves zig-zag (w, 7-w, 8+w, 15-w) so causal work is balanced.
-// K/V tiles of 64 keys are staged through double-buffered LDS (K rows padded to HD+8 floats:
+// Work split: a workgroup (4 waves) owns one (batch, KV head) pair's group of G query heads
+// (G = gcd(n_rep, 4): the heads that read the same K/V, so every staged K/V tile serves G heads)
+// and a range of queries.  Wave w works for head g = w % G; the 4/G waves of one head share its
+// 16-query blocks, dealt zig-zag (w, 7-w, 8+w, 15-w for 4 waves) so causal work is balanced.
+// K/V tiles of KT keys are staged through double-buffered LDS (K rows padded to HD+8 floats:
 // conflict-free ds_read_b128).  Tiles / 16-key groups past a block's last query are skipped.
 #pragma once
 #include "kernels.h"
@@ -28,42 +30,43 @@ namespace l3 {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int KT = 64;  // keys per LDS tile
-
-template <int HD, int QBW, bool VT = false>
+template <int HD, int QBW, int G, int KT>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
+    static_assert(HD % 16 == 0 && KT % 16 == 0 && (G == 1 || G == 2 || G == 4), "shape");
+    constexpr int WPH = 4 / G;                // waves per head
+    constexpr int NQB = QBW * WPH;            // 16-query blocks per head per workgroup
+    constexpr int QW = 16 * NQB;              // queries per workgroup
     constexpr int ND = HD / 16;               // 16-wide d groups
     constexpr int KSTR = HD + 8;              // == 8 mod 16 floats
-    // V image: row-major [key][d] read by ds_read_b32, or (VT) transposed [d][key] read by
-    // ds_read_b128 (four P.V sub-steps per read)
-    constexpr int VROWS = VT ? HD : KT;
-    constexpr int VSTR = VT ? KT + 8 : ((HD % 32 == 0) ? HD + 16 : HD);
-    constexpr int QW = 64 * QBW;              // queries per workgroup
+    constexpr int VSTR = (HD % 32 == 0) ? HD + 16 : HD;  // ds_read_b32 halves on distinct banks
     constexpr int K_F4 = KT * HD / 4;
     constexpr int K_IT = (K_F4 + 255) / 256;
+    constexpr int KG = KT / 16;               // 16-key groups per tile
 
     __shared__ __attribute__((aligned(16))) float Ks[2][KT][KSTR];
-    __shared__ __attribute__((aligned(16))) float Vs[2][VROWS][VSTR];
+    __shared__ __attribute__((aligned(16))) float Vs[2][KT][VSTR];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int kvh = h / (p.H / p.KVH);
+    const int g = wid % G, part = wid / G;
+    const int qt = blockIdx.x, b = blockIdx.z;
+    const int h = blockIdx.y * G + g;
+    const int kvh = (blockIdx.y * G) / (p.H / p.KVH);
     const int qdim = p.H * HD;
     const int fq = lane & 15;       // query within a 16-block
     const int fk = 4 * (lane >> 4); // k offset of this lane's operand quad
 
-    // this wave's q blocks (zig-zag) and their last query position
+    // this wave's q blocks (zig-zag over the WPH waves of its head)
     int qblk[QBW];
 #pragma unroll
-    for (int j = 0; j < QBW; ++j) qblk[j] = (j & 1) ? (8 * (j >> 1) + 7 - wid) : (8 * (j >> 1) + wid);
+    for (int j = 0; j < QBW; ++j)
+        qblk[j] = (j & 1) ? (2 * WPH * (j >> 1) + 2 * WPH - 1 - part) : (2 * WPH * (j >> 1) + part);
 
-    // queries of this workgroup: [q_lo, q_hi) local positions
+    const int start_pos = start_of(p);
     const int q_lo = qt * QW;
     const int q_hi = min(p.L, q_lo + QW);
-    const int key_end = p.start_pos + q_hi;  // keys [0, key_end) are needed
+    const int key_end = start_pos + q_hi;  // keys [0, key_end) are needed
     const int ntiles = (key_end + KT - 1) / KT;
 
-    // Q fragments in registers: qreg[j][dg] = Q[q][dg*16 + fk .. +3]
     f32x4 qreg[QBW][ND];
     f32x4 o[QBW][ND];
     float m_run[QBW], l_run[QBW];
@@ -105,14 +108,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             if (K_F4 % 256 == 0 || f < K_F4) {
                 const int row = f / (HD / 4), c = (f % (HD / 4)) * 4;
                 *reinterpret_cast<f32x4*>(&Ks[buf][row][c]) = rk[i];
-                if constexpr (VT) {
-                    Vs[buf][c + 0][row] = rv[i].x;
-                    Vs[buf][c + 1][row] = rv[i].y;
-                    Vs[buf][c + 2][row] = rv[i].z;
-                    Vs[buf][c + 3][row] = rv[i].w;
-                } else {
-                    *reinterpret_cast<f32x4*>(&Vs[buf][row][c]) = rv[i];
-                }
+                *reinterpret_cast<f32x4*>(&Vs[buf][row][c]) = rv[i];
             }
         }
     };
@@ -128,13 +124,13 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
         for (int j = 0; j < QBW; ++j) {
             const int qblock_first = q_lo + qblk[j] * 16;
             if (qblock_first >= p.L) continue;                        // padding block
-            const int qmax_abs = p.start_pos + min(qblock_first + 15, p.L - 1);
+            const int qmax_abs = start_pos + min(qblock_first + 15, p.L - 1);
             if (k0 > qmax_abs) continue;                              // whole tile masked
-            const int q_abs = p.start_pos + qblock_first + fq;
-            f32x4 sacc[4];
-            bool live[4];
+            const int q_abs = start_pos + qblock_first + fq;
+            f32x4 sacc[KG];
+            bool live[KG];
 #pragma unroll
-            for (int kg = 0; kg < 4; ++kg) {
+            for (int kg = 0; kg < KG; ++kg) {
                 live[kg] = (k0 + kg * 16) <= qmax_abs;                // wave-uniform
                 sacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (live[kg]) {
@@ -150,7 +146,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             // causal mask + tile max (lane holds keys k0 + kg*16 + fk + r for query q_abs)
             float mt = -INFINITY;
 #pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
+            for (int kg = 0; kg < KG; ++kg)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int key = k0 + kg * 16 + fk + r;
@@ -165,7 +161,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             m_run[j] = m_new;
             float psum = 0.f;
 #pragma unroll
-            for (int kg = 0; kg < 4; ++kg)
+            for (int kg = 0; kg < KG; ++kg)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float pv = exp2f(sacc[kg][r] - m_new);
@@ -176,23 +172,15 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
             for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;
 #pragma unroll
-            for (int kg = 0; kg < 4; ++kg) {
+            for (int kg = 0; kg < KG; ++kg) {
                 if (!live[kg]) continue;
 #pragma unroll
-                for (int dg = 0; dg < ND; ++dg) {
-                    if constexpr (VT) {
-                        const f32x4 vf = *reinterpret_cast<const f32x4*>(&Vs[cur][dg * 16 + fq][kg * 16 + fk]);
+                for (int dg = 0; dg < ND; ++dg)
 #pragma unroll
-                        for (int s = 0; s < 4; ++s)
-                            o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[s], sacc[kg][s], o[j][dg], 0, 0, 0);
-                    } else {
-#pragma unroll
-                        for (int s = 0; s < 4; ++s) {
-                            const float vf = Vs[cur][kg * 16 + fk + s][dg * 16 + fq];
-                            o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);
-                        }
+                    for (int s = 0; s < 4; ++s) {
+                        const float vf = Vs[cur][kg * 16 + fk + s][dg * 16 + fq];
+                        o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);
                     }
-                }
             }
         }
         if (tile + 1 < ntiles) sstore(cur ^ 1);

@@ -13,13 +13,37 @@ static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int EPI>
+static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
+    const int units = EPI == EPI_SWIGLU ? a.N / 2 : a.N;
+    const dim3 grid((unsigned)((units + 63) / 64)), block(256);
+    const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
+    const size_t lds = ((size_t)mr * a.K + 8) * 4;  // staged A rows + row sums
+    if (mr == 1) hipLaunchKernelGGL((gemv_kernel<EPI, 1>), grid, block, lds, s, a);
+    else if (mr == 2) hipLaunchKernelGGL((gemv_kernel<EPI, 2>), grid, block, lds, s, a);
+    else if (mr == 4) hipLaunchKernelGGL((gemv_kernel<EPI, 4>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((gemv_kernel<EPI, 8>), grid, block, lds, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return hipSuccess;
     if (a.K % 32 != 0 || a.K <= 0) return hipErrorInvalidValue;  // whole 32-deep k-tiles
     if (epi == EPI_SWIGLU && a.N % 32 != 0) return hipErrorInvalidValue;
     if (a.N % 4 != 0 || a.ldc % 4 != 0 || a.lda % 4 != 0) return hipErrorInvalidValue;  // 16-B rows
+    // M <= 8 (decode, short prompts): weight-streaming GEMV with the same epilogues
+    const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
+    if (a.M <= 8 && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS
+        switch (epi) {
+            case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);
+            case EPI_QKV: return launch_gemv<EPI_QKV>(a, s);
+            case EPI_RESID: return launch_gemv<EPI_RESID>(a, s);
+            case EPI_STORE: return launch_gemv<EPI_STORE>(a, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     // Configurations chosen with tools/gemm_tune (interleaved A/B on MI355X).
-    const bool small_m = a.M <= 32;  // decode / tiny M: 16 x 128 tile
+    const bool small_m = a.M <= 32;  // tiny M: 16 x 128 tile
     switch (epi) {
         case EPI_SWIGLU:  // 128 x 128, BK 16: 142 VGPRs + 48 KB LDS -> 3 blocks per CU
             if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2>(a, s);

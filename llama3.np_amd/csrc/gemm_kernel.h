@@ -136,7 +136,7 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, const float* stage
             // RoPE here, where a float4 holds two whole (even, odd) pairs: one 8-byte cos and
             // one 8-byte sin load per float4 (llama3.py:41-76), then q scaling / cache append
             const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
-            const int bidx = row / p.L, pos = p.start_pos + row - bidx * p.L;
+            const int bidx = row / p.L, pos = start_of(p) + row - bidx * p.L;
             const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
             const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
             const int head = cc / p.HD, d = cc - head * p.HD;
@@ -347,6 +347,117 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
             d[6] = xcc;
             d[7] = t;
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Skinny GEMM for M <= 8 rows (greedy decode, short prompts): the op is weight-streaming
+// (HBM / latency bound), so no LDS tiles and no MFMA.  A block (4 waves) stages the A rows
+// (times the RMSNorm weight) in LDS once; each wave owns 16 output units (a unit = one W row,
+// or a gate/up row pair for SwiGLU); lane (c = lane&15, kq = lane>>4) streams 16-byte pieces
+// k = 16i + 4kq of its unit's W row(s) straight to registers (all loads of a chunk issued
+// before the first use), the four k-quarters are summed with two shuffles, and lanes 0-15 run
+// the same epilogues as the tiled kernel.
+template <int EPI, int MR>
+__global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // [MR][K] then row sums [MR]
+    float* rsum = xs + MR * p.K;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int K4 = p.K / 4;
+    if (tid < MR) rsum[tid] = 0.f;
+    __syncthreads();
+    for (int f = tid; f < p.M * K4; f += 256) {
+        const int m = f / K4, k = (f - m * K4) * 4;
+        f32x4 v = *reinterpret_cast<const f32x4*>(p.A + (int64_t)m * p.lda + k);
+        if (p.norm) {
+            atomicAdd(&rsum[m], v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
+            v *= *reinterpret_cast<const f32x4*>(p.norm_w + k);
+        }
+        *reinterpret_cast<f32x4*>(xs + m * p.K + k) = v;
+    }
+    __syncthreads();
+
+    constexpr int ROWS = EPI == EPI_SWIGLU ? 2 : 1;   // W rows per unit
+    const int c = lane & 15, kq = lane >> 4;
+    const int unit = (blockIdx.x * 4 + wid) * 16 + c;
+    const int nunits = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
+    // W row(s) of this unit: SwiGLU unit u = hidden column u -> fused rows 32(u/16) + u%16 (+16)
+    int wrow[ROWS];
+    if constexpr (EPI == EPI_SWIGLU) {
+        wrow[0] = 32 * (unit / 16) + (unit % 16);
+        wrow[ROWS - 1] = wrow[0] + 16;
+    } else {
+        wrow[0] = unit;
+    }
+    const bool valid = unit < nunits;
+    float acc[ROWS][MR];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+        for (int m = 0; m < MR; ++m) acc[r][m] = 0.f;
+    constexpr int CH = 8;  // 16-byte pieces in flight per W row per lane
+    const int nk = p.K / 16;
+    for (int i0 = 0; i0 < nk; i0 += CH) {
+        f32x4 w[ROWS][CH];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+            for (int t = 0; t < CH; ++t) {
+                const int k = (i0 + t) * 16 + 4 * kq;
+                w[r][t] = (valid && i0 + t < nk)
+                              ? *reinterpret_cast<const f32x4*>(p.W + (int64_t)wrow[r] * p.K + k)
+                              : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const int k = (i0 + t) * 16 + 4 * kq;
+            if (i0 + t >= nk) break;
+#pragma unroll
+            for (int m = 0; m < MR; ++m) {
+                if (m >= p.M) break;
+                const f32x4 x = *reinterpret_cast<const f32x4*>(xs + m * p.K + k);
+#pragma unroll
+                for (int r = 0; r < ROWS; ++r)
+                    acc[r][m] += w[r][t].x * x.x + w[r][t].y * x.y + w[r][t].z * x.z + w[r][t].w * x.w;
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+        for (int m = 0; m < MR; ++m) {
+            acc[r][m] += __shfl_xor(acc[r][m], 16);
+            acc[r][m] += __shfl_xor(acc[r][m], 32);
+        }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+        if (m >= p.M) break;
+        const float sc = p.norm ? 1.0f / sqrtf(rsum[m] / (float)p.K + p.eps) : 1.0f;
+        if constexpr (EPI == EPI_QKV) {
+            const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
+            const int col = unit;
+            float v = acc[0][m] * sc;
+            const float partner = __shfl_xor(v, 1);  // RoPE pair partner: lane c ^ 1
+            if (kq == 0 && valid) {
+                const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
+                const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
+                const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
+                const int head = cc / p.HD, d = cc - head * p.HD;
+                if (is_q || is_k) {
+                    const int t = pos * (p.HD >> 1) + (d >> 1);
+                    const float cs = p.rope_cos[t], sn = p.rope_sin[t];
+                    v = (d & 1) ? (partner * sn + v * cs) : (v * cs - partner * sn);
+                }
+                if (is_q) p.q_out[(int64_t)m * qdim + col] = v * p.q_scale;
+                else (is_k ? p.cache_k : p.cache_v)[(((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d] = v;
+            }
+        } else if (kq == 0 && valid) {
+            float* dst = p.C + (int64_t)m * p.ldc + unit;
+            if constexpr (EPI == EPI_SWIGLU) *dst = silu_f(acc[0][m] * sc) * (acc[ROWS - 1][m] * sc);
+            else if constexpr (EPI == EPI_RESID) *dst += acc[0][m];
+            else *dst = acc[0][m] * sc;
         }
     }
 }

@@ -26,6 +26,7 @@ struct GemmArgs {
     float* cache_k; float* cache_v;// [maxB, KVH, Smax, HD]
     const float* rope_cos; const float* rope_sin;  // [Smax, HD/2]
     int L, start_pos, H, KVH, HD, Smax;
+    const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
     unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 8 per block
 };
@@ -36,13 +37,21 @@ struct AttnArgs {
     const float* cache_v;
     float* out;           // [B*L, H*HD]
     int B, L, start_pos, H, KVH, HD, Smax;
+    const int* pos_dev;   // if set, start_pos is read from device memory (graph replay)
 };
+
+// start position of a launch: the argument, or the device word a captured decode graph reads
+template <typename Args>
+__device__ __forceinline__ int start_of(const Args& p) {
+    return p.pos_dev ? *p.pos_dev : p.start_pos;
+}
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_embed(const int32_t* ids, const float* emb, float* h, int64_t T, int D,
                         hipStream_t s);
-hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s);
+hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
+                         int* pos_dev = nullptr);
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s);
 hipError_t launch_silu(const float* x, float* y, int64_t n, hipStream_t s);
 hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows, int dim,

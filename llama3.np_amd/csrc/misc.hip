@@ -31,7 +31,8 @@ __global__ void embed_kernel(const int32_t* __restrict__ ids, const float* __res
 }
 
 // argmax over each row with np.argmax's first-index tie-break (llama3.py:320).
-__global__ void argmax_kernel(const float* __restrict__ x, int n, int32_t* __restrict__ out) {
+__global__ void argmax_kernel(const float* __restrict__ x, int n, int32_t* __restrict__ out,
+                              int* __restrict__ pos_dev) {
     const float* row = x + (int64_t)blockIdx.x * n;
     float best = -INFINITY;
     int bi = 0x7fffffff;
@@ -59,7 +60,11 @@ __global__ void argmax_kernel(const float* __restrict__ x, int n, int32_t* __res
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) out[blockIdx.x] = si[0];
+    if (threadIdx.x == 0) {
+        out[blockIdx.x] = si[0];
+        // captured decode step: the next step runs one position later (llama3.py:312-318)
+        if (pos_dev && blockIdx.x == 0) *pos_dev += 1;
+    }
 }
 
 // row softmax (llama3.py:22-24): one wavefront per row, three passes over the row
@@ -135,8 +140,9 @@ hipError_t launch_embed(const int32_t* ids, const float* emb, float* h, int64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s) {
-    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(256), 0, s, logits, n, out);
+hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
+                         int* pos_dev) {
+    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(256), 0, s, logits, n, out, pos_dev);
     return hipGetLastError();
 }
 

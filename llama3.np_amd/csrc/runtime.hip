@@ -102,6 +102,16 @@ struct l3_ctx {
     // rccl
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // captured greedy decode step (llama3.py:316-320 as one hipGraph replay per token)
+    int32_t* dec_ids = nullptr;      // [maxB] input ids of the next decode step (argmax output)
+    int* dec_pos = nullptr;          // start_pos of the next decode step (argmax advances it)
+    int32_t* dec_host = nullptr;     // pinned [maxB] for the per-token ids copy-back
+    hipGraph_t dec_graph = nullptr;
+    hipGraphExec_t dec_exec = nullptr;
+    int dec_B = 0;                   // batch the graph was captured for
+    int64_t dec_pos_mirror = -1;     // host copy of *dec_pos; -1 = device decode state invalid
+    std::vector<int64_t> dec_last;   // ids the device state holds (last returned)
+    int64_t graph_steps = 0;         // decode steps served by graph replay (stats)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -147,10 +157,19 @@ static void dfree(void* p) {
     if (p) (void)hipFree(p);
 }
 
+static void drop_decode_graph(l3_ctx* c) {
+    if (c->dec_exec) (void)hipGraphExecDestroy(c->dec_exec);
+    if (c->dec_graph) (void)hipGraphDestroy(c->dec_graph);
+    c->dec_exec = nullptr;
+    c->dec_graph = nullptr;
+    c->dec_B = 0;
+}
+
 static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     const int64_t T = B * L;
     if (T <= c->ws_T && B <= c->ws_B) return 0;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    drop_decode_graph(c);  // the captured graph holds workspace pointers
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits);
     dfree(c->ids); dfree(c->amax);
     const int64_t Tn = T > c->ws_T ? T : c->ws_T;
@@ -257,6 +276,9 @@ extern "C" int l3_destroy(l3_ctx* c) {
     dfree(c->amax);
     for (void* p : c->scratch) dfree(p);
     for (auto& t : c->timers) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
+    drop_decode_graph(c);
+    dfree(c->dec_ids); dfree(c->dec_pos);
+    if (c->dec_host) (void)hipHostFree(c->dec_host);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -394,7 +416,7 @@ static int check_call(l3_ctx* c, int B, int L, int start_pos) {
 }
 
 // one transformer block on the residual stream c->h [B*L, D] (llama3.py:239-261)
-static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos) {
+static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* pos_dev = nullptr) {
     Layer& Ly = c->layers[li];
     const int64_t T = (int64_t)B * L;
     const int D = c->d.dim, FD = c->d.hidden_dim;
@@ -407,13 +429,14 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos) {
     g.rope_cos = c->rope_cos; g.rope_sin = c->rope_sin;
     g.L = L; g.start_pos = start_pos; g.H = c->d.n_heads; g.KVH = c->d.n_kv_heads; g.HD = c->HD;
     g.Smax = c->d.max_seq_len;
+    g.pos_dev = pos_dev;
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     if (timed(c, L3_K_QKV, [&] { return launch_gemm(EPI_QKV, g, c->stream); })) return 1;
     // causal attention over the cache
     AttnArgs a{};
     a.q = c->q; a.cache_k = Ly.cache_k; a.cache_v = Ly.cache_v; a.out = c->attn;
     a.B = B; a.L = L; a.start_pos = start_pos; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
-    a.HD = c->HD; a.Smax = c->d.max_seq_len;
+    a.HD = c->HD; a.Smax = c->d.max_seq_len; a.pos_dev = pos_dev;
     if (timed(c, L3_K_ATTN, [&] { return launch_attention(a, c->stream); })) return 1;
     // O-proj + residual (in place on h)
     GemmArgs o{};
@@ -435,13 +458,13 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos) {
 }
 
 static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
-                       float* logits_dev) {
+                       float* logits_dev, const int* pos_dev = nullptr) {
     const int64_t T = (int64_t)B * L;
     const int D = c->d.dim;
     if (timed(c, L3_K_EMBED, [&] { return launch_embed(ids_dev, c->emb, c->h, T, D, c->stream); }))
         return 1;
     for (int li = 0; li < (int)c->layers.size(); ++li)
-        if (run_layer(c, li, B, L, start_pos)) return 1;
+        if (run_layer(c, li, B, L, start_pos, pos_dev)) return 1;
     // final RMSNorm + lm_head on the last position of each sequence (llama3.py:304-307)
     GemmArgs lm{};
     lm.A = c->h + (int64_t)(L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
@@ -486,21 +509,73 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
     return 0;
 }
 
+// Capture one decode step (B sequences, L = 1) reading its position from dec_pos and its ids
+// from dec_ids; the argmax writes the next ids back into dec_ids and advances dec_pos.
+static int capture_decode_graph(l3_ctx* c, int B) {
+    drop_decode_graph(c);
+    const bool timing = c->timing;
+    c->timing = false;  // no event records inside the graph
+    HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    int rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
+    if (!rc) {
+        hipError_t e = launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, c->dec_pos);
+        if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
+    }
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    c->timing = timing;
+    if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
+    if (e != hipSuccess) return fail("hipStreamEndCapture failed: %s", hipGetErrorString(e));
+    e = hipGraphInstantiate(&c->dec_exec, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) { (void)hipGraphDestroy(g); return fail("hipGraphInstantiate failed: %s", hipGetErrorString(e)); }
+    c->dec_graph = g;
+    c->dec_B = B;
+    return 0;
+}
+
 extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
                                    int32_t start_pos, int64_t* next_ids_host, float* logits_host) {
     CHECK_CTX(c);
     if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
+    if (!c->dec_ids) {
+        HIP_TRY(hipMalloc(&c->dec_ids, (size_t)c->d.max_batch_size * 4));
+        HIP_TRY(hipMalloc(&c->dec_pos, sizeof(int)));
+        HIP_TRY(hipHostMalloc(&c->dec_host, (size_t)c->d.max_batch_size * 4));
+    }
+    // Graph replay when this call continues the device-resident decode state: one token per
+    // sequence at the position the state expects, fed the ids the previous step returned.
+    bool replay = L == 1 && !logits_host && c->dec_exec && c->dec_B == B &&
+                  c->dec_pos_mirror == start_pos && (int)c->dec_last.size() == B && !c->timing;
+    for (int i = 0; replay && i < B; ++i) replay = c->dec_last[(size_t)i] == ids_host[i];
+    if (replay) {
+        HIP_TRY(hipGraphLaunch(c->dec_exec, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->dec_host, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
+        c->dec_last.assign(next_ids_host, next_ids_host + B);
+        c->dec_pos_mirror = start_pos + 1;
+        c->graph_steps++;
+        return 0;
+    }
+    c->dec_pos_mirror = -1;
     if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
     if (forward_dev(c, c->ids, B, L, start_pos, c->logits)) return 1;
-    if (timed(c, L3_K_ARGMAX, [&] { return launch_argmax(c->logits, B, c->d.vocab_size, c->amax, c->stream); }))
+    if (timed(c, L3_K_ARGMAX, [&] { return launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream); }))
         return 1;
-    std::vector<int32_t> am((size_t)B);
-    HIP_TRY(hipMemcpyAsync(am.data(), c->amax, (int64_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->dec_host, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
     if (logits_host)
         HIP_TRY(hipMemcpyAsync(logits_host, c->logits, (int64_t)B * c->d.vocab_size * 4,
                                hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    for (int i = 0; i < B; ++i) next_ids_host[i] = am[(size_t)i];
+    for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
+    if (L == 1 && start_pos + 1 < c->d.max_seq_len) {
+        // arm the device state for the next decode step (one position later) and capture
+        const int next = start_pos + 1;
+        HIP_TRY(hipMemcpy(c->dec_pos, &next, sizeof(int), hipMemcpyHostToDevice));
+        if (c->dec_B != B && capture_decode_graph(c, B)) return 1;
+        c->dec_last.assign(next_ids_host, next_ids_host + B);
+        c->dec_pos_mirror = next;
+    }
     return 0;
 }
 

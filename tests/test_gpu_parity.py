@@ -209,3 +209,28 @@ def test_full_size_batch_rows_independent_and_match_oracle(tmpdir_mod):
         np.testing.assert_allclose(full[r:r + 1], alone, rtol=0, atol=1e-6)
         ref = orc.OracleModel(w, synth.stories15m(1))
         assert _close(full[r:r + 1], ref(ids[r:r + 1], 0)) <= 1e-4
+
+
+# ---- decode state / graph replay ------------------------------------------------------------
+
+def test_generate_twice_and_off_schedule_steps_match_oracle(tmpdir_mod):
+    """Two generate() calls on one model (caches persist, the decode graph is re-armed), then
+    greedy steps whose positions break the generate schedule (graph must not replay) — ids
+    exact vs the oracle doing the same sequence of calls."""
+    args = synth.tiny(2)
+    w, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, 5, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(21)
+    p1 = rng.integers(0, args.vocab_size, (2, 6))
+    p2 = rng.integers(0, args.vocab_size, (2, 4))
+    for prompt, n in ((p1, 40), (p2, 30)):
+        got = np.concatenate(list(m.generate(prompt, n)), axis=1)
+        np.testing.assert_array_equal(got, orc.greedy_ids(ref, prompt, n))
+    ctx = m.context
+    ids = np.array([[3], [5]])
+    for pos in (10, 11, 13, 12, 14):  # 11 follows 10 (replayable), 13 skips, 12 goes back
+        nxt, _ = ctx.greedy_step(ids, pos)
+        want = ref(ids, pos)[:, -1, :].argmax(-1)
+        np.testing.assert_array_equal(nxt, want)
+        ids = nxt.reshape(-1, 1)
