@@ -36,7 +36,7 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
         case 16: return launch_hd<16, 64, 4>(a, s);
         case 48: return launch_hd<48, 64, 4>(a, s);
         case 64: return launch_hd<64, 64, 4>(a, s);
-        case 128: return launch_hd<128, 32, 2>(a, s);  // KT 32: 72 KB LDS -> 2 workgroups per CU
+        case 128: return launch_hd<128, 32, 1>(a, s);  // KT 32: 72 KB LDS -> 2 workgroups per CU
         default: return hipErrorInvalidValue;
     }
 }
