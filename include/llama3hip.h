@@ -105,6 +105,12 @@ int l3_forward_dev(l3_ctx* ctx, const int32_t* ids_dev, int32_t B, int32_t L,
 int l3_greedy_step_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
                         int32_t start_pos, int64_t* next_ids_host, float* logits_host);
 
+/* The whole greedy loop on the device (same schedule and ids as Llama.generate,
+ * llama3.py:310-321, but not lazy: all max_new_tokens - L steps run, each one
+ * hipGraph replay, one copy-back at the end).  out_ids_host [B, max_new_tokens - L]. */
+int l3_greedy_generate_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
+                            int32_t max_new_tokens, int64_t* out_ids_host);
+
 /* ---- one block (replaces TransformerBlock.__call__, llama3.py:239-261) --- */
 /* x [B, L, D] fp32 host -> out [B, L, D]; uses and updates layer's KV cache. */
 int l3_layer_forward_host(l3_ctx* ctx, int32_t layer, const float* x_host, int32_t B,

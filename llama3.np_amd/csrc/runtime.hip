@@ -579,6 +579,55 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
     return 0;
 }
 
+// Whole greedy loop on the device (the reference's schedule, llama3.py:310-321): prefill at 0,
+// then decode step i >= 1 at pos = L + i, each step one replay of the captured decode graph;
+// ids accumulate on the device and come back with one copy at the end.  Not lazy: all
+// max_new_tokens - L steps run (Llama.generate keeps the reference's one-step-per-yield).
+extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
+                                       int32_t max_new_tokens, int64_t* out_ids_host) {
+    CHECK_CTX(c);
+    const int steps = max_new_tokens - L;
+    if (steps <= 0) return 0;
+    if (max_new_tokens - 1 > c->d.max_seq_len)
+        return fail("generate: last decode position %d exceeds max_seq_len %d", max_new_tokens - 1,
+                    c->d.max_seq_len);
+    std::vector<int64_t> first((size_t)B);
+    if (l3_greedy_step_host(c, ids_host, B, L, 0, first.data(), nullptr)) return 1;  // prefill
+    if (steps == 1) {
+        for (int b = 0; b < B; ++b) out_ids_host[(size_t)b * steps] = first[(size_t)b];
+        return 0;
+    }
+    // decode step 1 at pos L + 1 runs eagerly and arms the graph (device ids, pos = L + 2)
+    std::vector<int64_t> nxt((size_t)B);
+    if (l3_greedy_step_host(c, first.data(), B, 1, L + 1, nxt.data(), nullptr)) return 1;
+    int32_t* hist = nullptr;
+    HIP_TRY(hipMalloc(&hist, (size_t)steps * B * 4));
+    auto done = [&](int rc) { (void)hipStreamSynchronize(c->stream); (void)hipFree(hist); return rc; };
+    std::vector<int32_t> h32((size_t)B);
+    for (int b = 0; b < B; ++b) h32[(size_t)b] = (int32_t)first[(size_t)b];
+    if (hipMemcpy(hist, h32.data(), (size_t)B * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpyAsync(hist + B, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+        return done(fail("generate: history copy failed"));
+    for (int i = 2; i < steps; ++i) {
+        if (!c->dec_exec || c->dec_B != B) return done(fail("generate: decode graph not armed"));
+        if (hipGraphLaunch(c->dec_exec, c->stream) != hipSuccess ||
+            hipMemcpyAsync(hist + (size_t)i * B, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToDevice,
+                           c->stream) != hipSuccess)
+            return done(fail("generate: graph replay failed"));
+        c->graph_steps++;
+    }
+    std::vector<int32_t> all((size_t)steps * B);
+    if (hipMemcpyAsync(all.data(), hist, all.size() * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return done(fail("generate: copy-back failed"));
+    for (int i = 0; i < steps; ++i)
+        for (int b = 0; b < B; ++b) out_ids_host[(size_t)b * steps + i] = all[(size_t)i * B + b];
+    c->dec_last.assign(B, 0);
+    for (int b = 0; b < B; ++b) c->dec_last[(size_t)b] = all[(size_t)(steps - 1) * B + b];
+    c->dec_pos_mirror = L + steps;  // the device state now expects position L + steps
+    return done(0);
+}
+
 extern "C" int l3_layer_forward_host(l3_ctx* c, int32_t layer, const float* x_host, int32_t B,
                                      int32_t L, int32_t start_pos, float* out_host) {
     CHECK_CTX(c);

@@ -57,6 +57,7 @@ _SIGNATURES = {
     "l3_forward_dev": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
     "l3_greedy_step_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "l3_layer_forward_host": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P]),
+    "l3_greedy_generate_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
     "l3_attention_forward_host": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P]),
     "l3_op_softmax_host": (ctypes.c_int, [_P, _P, _I64, _I64, _P]),
     "l3_op_silu_host": (ctypes.c_int, [_P, _P, _I64, _P]),
@@ -178,6 +179,13 @@ class Context:
         check(lib().l3_greedy_step_host(self._h, ptr(ids), B, L, start_pos, ptr(nxt),
                                         ptr(logits) if logits is not None else None))
         return nxt, logits
+
+    def greedy_generate(self, ids: np.ndarray, max_new_tokens: int) -> np.ndarray:
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        B, L = ids.shape
+        out = np.empty((B, max(0, max_new_tokens - L)), np.int64)
+        check(lib().l3_greedy_generate_host(self._h, ptr(ids), B, L, max_new_tokens, ptr(out)))
+        return out
 
     def layer_forward(self, layer: int, x: np.ndarray, start_pos: int) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float32)

@@ -253,6 +253,14 @@ class Llama:
             next_id = nxt.reshape(-1, 1)
             yield next_id
 
+    def generate_all(self, input_ids, max_new_tokens: int) -> np.ndarray:
+        """Extension (not in the reference): the same greedy ids as ``generate`` —
+        same schedule, same decode hole — computed as one device-side loop of
+        graph-replayed steps with a single copy-back.  Returns int64
+        ``[B, max_new_tokens - L]``.  Unlike ``generate`` it is not lazy: every step
+        runs, so use it when the caller consumes all tokens."""
+        return self._ctx.greedy_generate(np.asarray(input_ids), max_new_tokens)
+
 
 def main(argv=None, tokenizer_path="./tokenizer.model.np", model_path="./stories15M.model.npz"):
     """CLI of reference llama3.py:324-349: stream greedy tokens for a prompt, stop on

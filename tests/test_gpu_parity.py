@@ -139,6 +139,10 @@ def test_stories15m_greedy_dream_exact(tmpdir_mod, preset):
     m = llama3.Llama(path, args)
     ids = np.concatenate(list(m.generate(g["dream_prompt"], int(g["dream_max_new"]))), axis=1)
     np.testing.assert_array_equal(ids, g["dream_ids"])
+    # the device-side loop (extension) must give the same ids, also on a model whose caches
+    # already hold a previous generation (the hole and stale slots behave as in the reference)
+    np.testing.assert_array_equal(m.generate_all(g["dream_prompt"], int(g["dream_max_new"])),
+                                  g["dream_ids"])
 
 
 def test_stories15m_live_oracle_gqa_batch(tmpdir_mod):
