@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                     }
             }
         } else {
-    #pragma unroll
+#pragma unroll
             for (int j = 0; j < QBW; ++j) {
                 const int qblock_first = q_lo + qblk[j] * 16;
                 if (qblock_first >= p.L) continue;                        // padding block
@@ -212,54 +212,61 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 const int q_abs = start_pos + qblock_first + fq;
                 f32x4 sacc[KG];
                 bool live[KG];
-    #pragma unroll
+#pragma unroll
                 for (int kg = 0; kg < KG; ++kg) {
                     live[kg] = (k0 + kg * 16) <= qmax_abs;                // wave-uniform
                     sacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
                     if (live[kg]) {
-    #pragma unroll
+#pragma unroll
                         for (int dg = 0; dg < ND; ++dg) {
                             const f32x4 kf = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
-    #pragma unroll
+#pragma unroll
                             for (int s = 0; s < 4; ++s)
                                 sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
                         }
                     }
                 }
-                // causal mask + tile max (lane holds keys k0 + kg*16 + fk + r for query q_abs)
+                // causal mask (diagonal tiles only) + tile max; lane holds keys
+                // k0 + kg*16 + fk + r for query q_abs
+                const bool diag = k0 + KT - 1 > start_pos + qblock_first;  // wave-uniform
                 float mt = -INFINITY;
-    #pragma unroll
+#pragma unroll
                 for (int kg = 0; kg < KG; ++kg)
-    #pragma unroll
+#pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const int key = k0 + kg * 16 + fk + r;
-                        const float v = (live[kg] && key <= q_abs) ? sacc[kg][r] : -INFINITY;
+                        float v = sacc[kg][r];
+                        if (diag) {
+                            const int key = k0 + kg * 16 + fk + r;
+                            v = (live[kg] && key <= q_abs) ? v : -INFINITY;
+                        }
                         sacc[kg][r] = v;
                         mt = fmaxf(mt, v);
                     }
                 mt = fmaxf(mt, __shfl_xor(mt, 16));
                 mt = fmaxf(mt, __shfl_xor(mt, 32));
                 const float m_new = fmaxf(m_run[j], mt);
-                const float alpha = exp2f(m_run[j] - m_new);   // 0 on the first tile
+                // v_exp_f32 directly: arguments are <= 0 (exact 0 at -inf), so the libm
+                // denormal-range guard around exp2f is dead weight (5 VALU per call)
+                const float alpha = __builtin_amdgcn_exp2f(m_run[j] - m_new);  // 0 on the first tile
                 m_run[j] = m_new;
                 float psum = 0.f;
-    #pragma unroll
+#pragma unroll
                 for (int kg = 0; kg < KG; ++kg)
-    #pragma unroll
+#pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float pv = exp2f(sacc[kg][r] - m_new);
+                        const float pv = __builtin_amdgcn_exp2f(sacc[kg][r] - m_new);
                         sacc[kg][r] = pv;
                         psum += pv;
                     }
                 l_run[j] = l_run[j] * alpha + psum;
-    #pragma unroll
+#pragma unroll
                 for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;
-    #pragma unroll
+#pragma unroll
                 for (int kg = 0; kg < KG; ++kg) {
                     if (!live[kg]) continue;
-    #pragma unroll
+#pragma unroll
                     for (int dg = 0; dg < ND; ++dg)
-    #pragma unroll
+#pragma unroll
                         for (int s = 0; s < 4; ++s) {
                             const float vf = Vs[cur][kg * 16 + fk + s][dg * 16 + fq];
                             o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);

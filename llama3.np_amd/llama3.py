@@ -93,6 +93,21 @@ def _check_freqs(freqs_cos, freqs_sin, L: int, head_dim: int) -> None:
             raise ValueError(f"freqs shape {np.shape(f)} does not match (L={L}, HD/2={head_dim // 2})")
 
 
+class _Dropped:
+    """Placeholder for a host weight not kept by a streaming load (keep_host_weights=False):
+    the tensor lives only in HBM; host-side uses of it raise."""
+
+    def __init__(self, shape):
+        self.shape = tuple(shape)
+
+    @property
+    def T(self):
+        return _Dropped(self.shape[::-1])
+
+    def __array__(self, *a, **k):
+        raise RuntimeError("host copy not kept (Llama(..., keep_host_weights=False))")
+
+
 class FeedForward:
     """SwiGLU MLP (reference llama3.py:86-103): one fused gate|up MFMA GEMM with a
     silu(g)*u epilogue, then the down GEMM."""
@@ -160,7 +175,8 @@ class TransformerBlock:
     """Pre-norm block (reference llama3.py:216-261) executed as 4 MFMA GEMMs with
     fused epilogues plus one fused attention kernel (kernel list)."""
 
-    def __init__(self, weight: dict, layer_id: int, args: ModelArgs, _bind: Optional[tuple] = None):
+    def __init__(self, weight: dict, layer_id: int, args: ModelArgs, _bind: Optional[tuple] = None,
+                 _keep_host: bool = True):
         p = f"model.layers.{layer_id}."
         names = {
             l3hip.W_Q: p + "self_attn.q_proj.weight", l3hip.W_K: p + "self_attn.k_proj.weight",
@@ -187,6 +203,8 @@ class TransformerBlock:
             self._ctx.upload(self._layer, kind, t)
         if standalone:
             self._ctx.finalize()
+        if not _keep_host:  # streaming load: the device copy is the only copy
+            w = {k: _Dropped(v.shape) for k, v in w.items()}
         self.attention = Attention(w[l3hip.W_Q], w[l3hip.W_K], w[l3hip.W_V], w[l3hip.W_O], args,
                                    _bind=_bind)
         self.feed_forward = FeedForward(w[l3hip.W_UP], w[l3hip.W_GATE], w[l3hip.W_DOWN])
@@ -207,23 +225,34 @@ class Llama:
     device-resident across all layers and copies back only the last-position
     logits.  ``generate`` runs argmax on the device and copies back only ids."""
 
-    def __init__(self, model_path: str, args: ModelArgs, device: Optional[int] = None):
+    def __init__(self, model_path: str, args: ModelArgs, device: Optional[int] = None,
+                 keep_host_weights: bool = True):
+        """``device`` / ``keep_host_weights`` are extensions.  With
+        ``keep_host_weights=False`` every ``.npz`` member is read, uploaded to HBM and
+        dropped before the next is read (NumPy's NpzFile reads members lazily), so host
+        memory peaks at one tensor instead of the whole checkpoint (32 GB for the
+        Llama-3-8B shape); the reference-style host attributes then hold placeholders."""
         self.args = args
+        keep = keep_host_weights
         weight = load_parameters(model_path)
-        self.tok_embedding = weight.get("model.embed_tokens.weight")
         self.freqs_cos, self.freqs_sin = compute_cos_sin_cache(args.dim // args.n_heads,
                                                                args.max_seq_len)
         hidden = weight.get("model.layers.0.mlp.gate_proj.weight").shape[0]
         dev = DEFAULT_DEVICE if device is None else device
         self._ctx = l3hip.Context(_dims(args, hidden, args.n_layers, args.vocab_size), dev)
-        self._ctx.upload(0, l3hip.W_EMBED, self.tok_embedding)
-        self.layers = [TransformerBlock(weight, i, args, _bind=(self._ctx, i))
+        emb = weight.get("model.embed_tokens.weight")
+        self._ctx.upload(0, l3hip.W_EMBED, emb)
+        self.tok_embedding = emb if keep else _Dropped(emb.shape)
+        del emb
+        self.layers = [TransformerBlock(weight, i, args, _bind=(self._ctx, i), _keep_host=keep)
                        for i in range(args.n_layers)]
-        self.norm = RMSNorm(weight.get("model.norm.weight"), eps=args.norm_eps)
+        norm_w = weight.get("model.norm.weight")
+        self.norm = RMSNorm(norm_w, eps=args.norm_eps)
+        self._ctx.upload(0, l3hip.W_FINAL_NORM, norm_w)
         lm = weight.get("lm_head.weight")
-        self.lm_head_weight = lm.T
-        self._ctx.upload(0, l3hip.W_FINAL_NORM, self.norm.weight)
         self._ctx.upload(0, l3hip.W_LM_HEAD, lm)
+        self.lm_head_weight = lm.T if keep else _Dropped(lm.shape[::-1])
+        del lm
         self._ctx.finalize()
         del weight
 

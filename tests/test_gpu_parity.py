@@ -145,6 +145,18 @@ def test_stories15m_greedy_dream_exact(tmpdir_mod, preset):
                                   g["dream_ids"])
 
 
+def test_streaming_load_matches(tmpdir_mod):
+    """keep_host_weights=False (read -> upload -> drop per tensor) gives identical logits."""
+    args = synth.tiny(2)
+    _, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, 7, "sharp")
+    ids = np.random.default_rng(2).integers(0, args.vocab_size, (2, 9))
+    a = llama3.Llama(path, args)(ids, 0)
+    m = llama3.Llama(path, args, keep_host_weights=False)
+    np.testing.assert_array_equal(m(ids, 0), a)
+    with pytest.raises(RuntimeError, match="host copy not kept"):
+        np.asarray(m.tok_embedding)
+
+
 def test_stories15m_live_oracle_gqa_batch(tmpdir_mod):
     """Live oracle at a size not in the fixtures: B=3, L=80 prefill then a 7-token chunk."""
     args = synth.stories15m(3)
