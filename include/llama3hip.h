@@ -149,7 +149,9 @@ int l3_d2h(l3_ctx* ctx, void* dst_host, const void* src_dev, size_t bytes);
 int l3_synchronize(l3_ctx* ctx);
 
 /* ---- kernel timing (HIP events on the context stream) -------------------- */
-int l3_kernel_timing(l3_ctx* ctx, int32_t enable);    /* also resets the stats */
+/* mask: bit k = record HIP events around launches of l3_kernel_id k (0 = off);
+ * also resets the stats */
+int l3_kernel_timing(l3_ctx* ctx, int32_t mask);
 /* total milliseconds and launch count per l3_kernel_id since last reset */
 int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
 

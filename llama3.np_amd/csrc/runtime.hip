@@ -93,8 +93,9 @@ struct l3_ctx {
     int32_t *ids = nullptr, *amax = nullptr;
     // op scratch
     std::vector<void*> scratch;
-    // timing
+    // timing (bit k of timing_mask: record HIP events around launches of kernel id k)
     bool timing = false;
+    unsigned timing_mask = 0;
     std::vector<Timer> timers;
     size_t timer_used = 0;
     double tot_ms[L3_K_COUNT] = {0};
@@ -123,7 +124,7 @@ static int set_dev(l3_ctx* c) {
 template <typename F>
 static int timed(l3_ctx* c, int kind, F&& launch) {
     Timer* t = nullptr;
-    if (c->timing) {
+    if (c->timing && (c->timing_mask >> kind & 1u)) {
         if (c->timer_used == c->timers.size()) {
             Timer nt{};
             HIP_TRY(hipEventCreate(&nt.a));
@@ -192,7 +193,7 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 1;
+    if (minor) *minor = 2;  // bumped whenever a hot kernel changes (keys profiles/pmc_*.json)
     return 0;
 }
 
@@ -855,6 +856,7 @@ extern "C" int l3_kernel_timing(l3_ctx* c, int32_t enable) {
     c->timer_used = 0;
     for (int k = 0; k < L3_K_COUNT; ++k) { c->tot_ms[k] = 0; c->cnt[k] = 0; }
     c->timing = enable != 0;
+    c->timing_mask = (unsigned)enable;
     return 0;
 }
 

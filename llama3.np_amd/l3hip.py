@@ -224,8 +224,14 @@ class Context:
     def synchronize(self) -> None:
         check(lib().l3_synchronize(self._h))
 
-    def kernel_timing(self, enable: bool) -> None:
-        check(lib().l3_kernel_timing(self._h, 1 if enable else 0))
+    def kernel_timing(self, enable, kernels=None) -> None:
+        """Record HIP events around launches (all kernels, or only the named ones)."""
+        mask = 0
+        if enable:
+            names = KERNELS if kernels is None else kernels
+            for k in names:
+                mask |= 1 << KERNELS.index(k)
+        check(lib().l3_kernel_timing(self._h, mask))
 
     def kernel_stats(self) -> dict:
         ms = np.zeros(len(KERNELS), np.float64)

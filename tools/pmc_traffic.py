@@ -12,6 +12,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
@@ -39,12 +40,14 @@ def main():
         kernels[k] = {"launches": len(fe[k]), "fetch_kib_raw": round(f_kib, 1),
                       "write_kib": round(w_kib, 1),
                       "hbm_bytes_per_launch": int((2 * f_kib + w_kib) * 1024)}
-    gu = [k for k in kernels if "gemm_nt_kernel<2, 2, 4, 4, 2>" in k]
+    # the gate|up GEMM is the gemm kernel instantiated with EPI_SWIGLU (5th template argument 2)
+    gu = [k for k in kernels if re.search(r"gemm_\w+_kernel<\d+, \d+, \d+, \d+, 2[,>]", k)]
     algo = 4 * (ROWS * D + 2 * FD * D + ROWS * FD)
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
                      "python bench.py --steps 2 --warmup 1",
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
            "workload_rows": ROWS,
+           "lib_version": sys.argv[4] if len(sys.argv) > 4 else None,
            "gateup_kernel": gu[0] if gu else None,
            "hbm_bytes_per_launch": kernels[gu[0]]["hbm_bytes_per_launch"] if gu else None,
            "algorithmic_bytes_per_launch": algo,

@@ -9,23 +9,26 @@ per-kernel calls, mean duration and algorithmic TFLOP/s at the stories15M C3 sha
 import argparse
 import csv
 import json
+import re
 import shutil
 
 D, FD, H, HD, VS, L = 288, 768, 6, 48, 32000, 256
 
 def flops(name, T):
-    if "gemm_nt_kernel<2, 2, 4, 4, 2>" in name:
-        return "gate|up (SwiGLU)", 2.0 * T * D * 2 * FD
-    if "gemm_nt_kernel<2, 2, 4, 3, 3>" in name:
-        return "QKV (+RMSNorm, RoPE, KV append)", 2.0 * T * D * 3 * D
-    if "gemm_nt_kernel<2, 2, 4, 3, 1>" in name:
-        return "O-proj + down (+residual), mixed", None
+    """Role and algorithmic FLOPs of a kernel at the C3 shape, from its template arguments."""
+    m = re.search(r"gemm_\w+_kernel<(\d+), (\d+), (\d+), (\d+), (\d+)", name)
+    if m:
+        wm, wn, tm, tn, epi = map(int, m.groups())
+        if epi == 2:
+            return "gate|up (SwiGLU)", 2.0 * T * D * 2 * FD
+        if epi == 3:
+            return "QKV (+RMSNorm, RoPE, KV append)", 2.0 * T * D * 3 * D
+        if epi == 1:  # dispatch: 64x96 at K = 288 (O-proj), 128x96 at K = 768 (down)
+            return ("O-proj (+residual)", 2.0 * T * D * D) if tm == 2 else ("down (+residual)", 2.0 * T * FD * D)
+        if epi == 0:
+            return "lm_head (+final RMSNorm, last row)", 2.0 * (T // L) * D * VS
     if "attn_fwd_kernel" in name:
-        B = T // L
-        return "causal attention (useful half)", 2.0 * 2 * H * HD * L * (L + 1) / 2 * B
-    if "gemm_nt_kernel<2, 2, 4, 4, 0>" in name:
-        B = T // L
-        return "lm_head (+final RMSNorm, last row)", 2.0 * B * D * VS
+        return "causal attention (useful half)", 2.0 * 2 * H * HD * L * (L + 1) / 2 * (T // L)
     return name.split("(")[0], None
 
 def main():
