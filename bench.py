@@ -42,8 +42,9 @@ B_PER_GPU, SEQ = 256, 256
 
 
 class Dist:
-    """Harness-side rendezvous (gloo on the host) for the RCCL id, barriers and the
-    max-over-ranks time.  The data-path collective is RCCL inside libllama3hip."""
+    """One process per GPU (torchrun env).  No PyTorch in this process: the RCCL id goes
+    rank 0 -> peers through an atomically renamed file (single node, keyed by the launcher's
+    pid and MASTER_PORT), and barriers / the max-over-ranks time run over RCCL itself."""
 
     def __init__(self, n):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -51,32 +52,27 @@ class Dist:
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         if n != self.world:
             raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}; launch N>1 with torch.distributed.run")
-        self.pg = None
+        self.ctx = None
+
+    def init_comm(self, ctx):
+        self.ctx = ctx
         if self.world > 1:
-            import torch.distributed as dist  # host-side rendezvous only (gloo)
-
-            dist.init_process_group("gloo")
-            self.dist = dist
-
-    def bcast_bytes(self, b):
-        if self.world == 1:
-            return b
-        obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
-        return obj[0]
+            key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+            uid = l3hip.exchange_unique_id(self.rank, self.world, key)
+            ctx.comm_init(self.world, self.rank, uid)
+            ctx.comm_barrier()
+            if self.rank == 0:  # every rank has read the id once the barrier completed
+                try:
+                    os.remove(os.path.join("/tmp", f"l3_rccl_uid_{key}"))
+                except OSError:
+                    pass
 
     def barrier(self):
         if self.world > 1:
-            self.dist.barrier()
+            self.ctx.comm_barrier()
 
     def max(self, x):
-        if self.world == 1:
-            return x
-        import torch
-
-        t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
-        return float(t.item())
+        return self.ctx.comm_max(x) if self.world > 1 else x
 
 
 def cpu_baseline():
@@ -228,11 +224,9 @@ def main():
     logits_dev = ctx.alloc(B_PER_GPU * VS * 4)
     gathered_dev = None
     rows = [B_PER_GPU] * dist.world
-    if dist.world > 1:
-        uid = dist.bcast_bytes(l3hip.comm_unique_id() if dist.rank == 0 else None)
-        ctx.comm_init(dist.world, dist.rank, uid)
-        if dist.rank == 0:
-            gathered_dev = ctx.alloc(B_PER_GPU * dist.world * VS * 4)
+    dist.init_comm(ctx)
+    if dist.world > 1 and dist.rank == 0:
+        gathered_dev = ctx.alloc(B_PER_GPU * dist.world * VS * 4)
 
     def step():
         ctx.forward_dev(ids_dev, B_PER_GPU, SEQ, 0, logits_dev)

@@ -164,6 +164,8 @@ int l3_comm_init(l3_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128
 int l3_comm_gather_logits(l3_ctx* ctx, const float* src_dev, float* dst_dev,
                           const int64_t* rows_per_rank, int32_t root);
 int l3_comm_barrier(l3_ctx* ctx);
+/* max over ranks of one host double (in place; synchronous) — e.g. step time */
+int l3_comm_allreduce_max(l3_ctx* ctx, double* value);
 
 #ifdef __cplusplus
 }

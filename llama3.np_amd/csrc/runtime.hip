@@ -920,6 +920,24 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
     return 0;
 }
 
+extern "C" int l3_comm_allreduce_max(l3_ctx* c, double* value) {
+    CHECK_CTX(c);
+    if (!c->comm) return fail("l3_comm_allreduce_max: communicator not initialised");
+    if (set_dev(c)) return 1;
+    double* d = nullptr;
+    HIP_TRY(hipMalloc(&d, sizeof(double)));
+    hipError_t e = hipMemcpyAsync(d, value, sizeof(double), hipMemcpyHostToDevice, c->stream);
+    ncclResult_t r = e == hipSuccess ? ncclAllReduce(d, d, 1, ncclFloat64, ncclMax, c->comm, c->stream)
+                                     : ncclSuccess;
+    if (e == hipSuccess && r == ncclSuccess)
+        e = hipMemcpyAsync(value, d, sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (r != ncclSuccess) return fail("ncclAllReduce(max) failed: %s", ncclGetErrorString(r));
+    if (e != hipSuccess) return fail("allreduce_max copy failed: %s", hipGetErrorString(e));
+    return 0;
+}
+
 extern "C" int l3_comm_barrier(l3_ctx* c) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_barrier: communicator not initialised");

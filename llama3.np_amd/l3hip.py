@@ -76,6 +76,7 @@ _SIGNATURES = {
     "l3_comm_init": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "l3_comm_gather_logits": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
     "l3_comm_barrier": (ctypes.c_int, [_P]),
+    "l3_comm_allreduce_max": (ctypes.c_int, [_P, _P]),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -251,6 +252,11 @@ class Context:
     def comm_barrier(self) -> None:
         check(lib().l3_comm_barrier(self._h))
 
+    def comm_max(self, x: float) -> float:
+        v = ctypes.c_double(x)
+        check(lib().l3_comm_allreduce_max(self._h, ctypes.byref(v)))
+        return v.value
+
     # ---- ops ----
     def op_softmax(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float32)
@@ -300,6 +306,34 @@ class Context:
         check(lib().l3_op_ffn_host(self._h, ptr(x), x.size // D, D, FD, ptr(wg), ptr(wu), ptr(wd),
                                    ptr(y)))
         return y
+
+
+def exchange_unique_id(rank: int, world: int, key: str, timeout_s: float = 120.0) -> bytes:
+    """Ship the 128-byte RCCL id from rank 0 to the other ranks of ONE node through an
+    atomically renamed file in /tmp (no PyTorch / gloo needed).  ``key`` must be unique per
+    launch and equal on all ranks (e.g. launcher pid + MASTER_PORT)."""
+    import time
+
+    path = os.path.join("/tmp", f"l3_rccl_uid_{key}")
+    if rank == 0:
+        uid = comm_unique_id()
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+        return uid
+    t0 = time.time()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                uid = f.read()
+            if len(uid) == 128:
+                return uid
+        except FileNotFoundError:
+            pass
+        if time.time() - t0 > timeout_s:
+            raise RuntimeError(f"timed out waiting for the RCCL id at {path}")
+        time.sleep(0.01)
 
 
 def comm_unique_id() -> bytes:

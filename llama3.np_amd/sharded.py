@@ -58,14 +58,23 @@ class ShardedPrefill:
 
     @classmethod
     def on_device(cls, model, world: int, rank: int,
-                  bcast_uid: Callable[[Optional[bytes]], bytes], root: int = 0):
+                  bcast_uid: Optional[Callable[[Optional[bytes]], bytes]] = None, root: int = 0):
         """Wire to a ``llama3.Llama`` on this rank's GPU.  ``bcast_uid`` ships the
-        128-byte RCCL id from the root to every rank (any host-side channel)."""
+        128-byte RCCL id from the root to every rank (any host-side channel); by default a
+        file hand-off in /tmp keyed by the launcher pid and MASTER_PORT (one node)."""
+        import os
+
         import l3hip
 
         ctx = model.context
         VS = ctx.dims.vocab_size
-        uid = bcast_uid(l3hip.comm_unique_id() if rank == root else None)
+        if bcast_uid is None:
+            if root != 0:
+                raise ValueError("the default id exchange needs root 0")
+            key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+            uid = l3hip.exchange_unique_id(rank, world, key)
+        else:
+            uid = bcast_uid(l3hip.comm_unique_id() if rank == root else None)
         ctx.comm_init(world, rank, uid)
         bufs = {}
 

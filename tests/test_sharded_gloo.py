@@ -88,3 +88,29 @@ def test_sharded_prefill_gloo(world, tmp_path):
     mp.spawn(_worker, args=(world, _free_port(), cases, str(tmp_path)), nprocs=world, join=True)
     ok = np.load(tmp_path / "ok.npy")
     assert ok.all(), ok
+
+
+def _uid_worker(rank, world, key, outdir):
+    import l3hip
+
+    l3hip.comm_unique_id = lambda: bytes(range(7, 135))  # stand-in id (no RCCL bootstrap)
+    uid = l3hip.exchange_unique_id(rank, world, key, timeout_s=30)
+    with open(os.path.join(outdir, f"uid{rank}"), "wb") as f:
+        f.write(uid)
+
+
+def test_unique_id_file_exchange(tmp_path):
+    """bench.py's torch-free RCCL id hand-off: every rank reads rank 0's 128 bytes."""
+    import multiprocessing as mp
+
+    key = f"test_{os.getpid()}_{_free_port()}"
+    ctx = mp.get_context("spawn")
+    ps = [ctx.Process(target=_uid_worker, args=(r, 3, key, str(tmp_path))) for r in (2, 1, 0)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    got = [(tmp_path / f"uid{r}").read_bytes() for r in range(3)]
+    assert got[0] == bytes(range(7, 135)) and got[1] == got[0] and got[2] == got[0]
+    os.remove(os.path.join("/tmp", f"l3_rccl_uid_{key}"))
