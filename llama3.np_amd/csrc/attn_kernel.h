@@ -38,7 +38,10 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     constexpr int QW = 16 * NQB;              // queries per workgroup
     constexpr int ND = HD / 16;               // 16-wide d groups
     constexpr int KSTR = HD + 8;              // == 8 mod 16 floats
-    constexpr int VSTR = (HD % 32 == 0) ? HD + 16 : HD;  // ds_read_b32 halves on distinct banks
+    // P.V reads V[key = kg*16 + 4(lane>>4) + s][d = dg*16 + (lane&15)] with ds_read_b32: lanes
+    // 0-15 and 16-31 (one bank group) are 4 rows apart, so 4*VSTR must be == 16 (mod 32):
+    // VSTR == 4 (mod 8) puts the two 16-lane halves on disjoint banks (HD is a multiple of 16)
+    constexpr int VSTR = HD + 4;
     constexpr int K_F4 = KT * HD / 4;
     constexpr int K_IT = (K_F4 + 255) / 256;
     constexpr int KG = KT / 16;               // 16-key groups per tile

@@ -25,6 +25,10 @@ for s in "$@"; do
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown ;;
     tune) step tune 600 tools/gemm_tune 5 10 ;;
     tunec5) step tunec5 900 tools/gemm_tune 3 3 c5 ;;
+    pmcsq) step pmcA 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcA -o run --output-format csv -- tools/attn_tune 1 2
+           step pmcB 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcB -o run --output-format csv -- tools/attn_tune 1 2
+           step pmcC 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcC -o run --output-format csv -- tools/gemm_tune 1 2
+           step pmcD 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcD -o run --output-format csv -- tools/gemm_tune 1 2 ;;
     stamps) step stamps 300 tools/gemm_tune 1 1 stamps ;;
     attntune) step attntune 600 tools/attn_tune ;;
     decode) step decode 300 python tools/bench_decode.py ;;
