@@ -904,9 +904,14 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
         for (int r = 0; r < c->nranks; ++r) {
             const int64_t n = rows_per_rank[r] * VS;
             if (r == root) {
-                if (n && dst_dev + off * VS != src_dev)
-                    HIP_TRY(hipMemcpyAsync(dst_dev + off * VS, src_dev, n * 4, hipMemcpyDeviceToDevice,
-                                           c->stream));
+                if (n && dst_dev + off * VS != src_dev) {
+                    const hipError_t e = hipMemcpyAsync(dst_dev + off * VS, src_dev, n * 4,
+                                                        hipMemcpyDeviceToDevice, c->stream);
+                    if (e != hipSuccess) {
+                        (void)ncclGroupEnd();  // close the group before reporting
+                        return fail("gather root copy: %s", hipGetErrorString(e));
+                    }
+                }
             } else if (n) {
                 NCCL_TRY(ncclRecv(dst_dev + off * VS, (size_t)n, ncclFloat32, r, c->comm, c->stream));
             }
@@ -947,6 +952,7 @@ extern "C" int l3_comm_barrier(l3_ctx* c) {
     else {
         HIP_TRY(hipMalloc(&one, 4));
         c->scratch.push_back(one);
+        HIP_TRY(hipMemsetAsync(one, 0, 4, c->stream));  // the sum stays 0: no inf/NaN over time
     }
     NCCL_TRY(ncclAllReduce(one, one, 1, ncclFloat32, ncclSum, c->comm, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));

@@ -252,3 +252,20 @@ def test_generate_twice_and_off_schedule_steps_match_oracle(tmpdir_mod):
         want = ref(ids, pos)[:, -1, :].argmax(-1)
         np.testing.assert_array_equal(nxt, want)
         ids = nxt.reshape(-1, 1)
+
+
+def test_generate_all_batched_matches_oracle(tmpdir_mod):
+    """the batched (B>1) device-side greedy loop — hole semantics, on-device
+    argmax — gives the reference's ids for every row, on the GQA tiny model (B=3) and on
+    stories15M (B=4), the second call running on caches the first one left behind."""
+    for args, hidden, seed, shape, n in ((synth.tiny(3), synth.TINY_HIDDEN, 11, (3, 5), 48),
+                                         (synth.stories15m(4), synth.STORIES15M_HIDDEN, 0, (4, 7), 40)):
+        w, path = _model(tmpdir_mod, args, hidden, seed, "sharp")
+        m = llama3.Llama(path, args)
+        ref = orc.OracleModel(w, args)
+        rng = np.random.default_rng(seed + 1)
+        for _ in range(2):
+            prompt = rng.integers(0, args.vocab_size, shape)
+            got = m.generate_all(prompt, n)
+            assert got.dtype == np.int64 and got.shape == (shape[0], n - shape[1])
+            np.testing.assert_array_equal(got, orc.greedy_ids(ref, prompt, n))

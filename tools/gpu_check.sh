@@ -35,6 +35,7 @@ for s in "$@"; do
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
     c5small) step c5small 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
+    rccl1) step rccl1 180 python tools/rccl_selftest.py --world 1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
