@@ -84,9 +84,11 @@ int l3_destroy(l3_ctx* ctx);
 int l3_upload_weight(l3_ctx* ctx, int32_t layer, int32_t kind, const float* host,
                      int64_t rows, int64_t cols);
 /* Mark the upload phase complete (QKV and gate/up are fused at upload time:
- * q|k|v rows stacked, gate/up interleaved in 16-row groups).  Must be called
- * once after the uploads, before any forward; entry points check that the
- * tensors they need were uploaded. */
+ * q|k|v rows stacked, gate/up interleaved in 16-row groups).  Folds each
+ * RMSNorm weight into the columns of the GEMM that consumes the normalised
+ * rows (attention norm -> QKV, FFN norm -> gate/up, final norm -> lm_head)
+ * where both were uploaded.  Must be called once after the uploads, before
+ * any forward; entry points check that the tensors they need were uploaded. */
 int l3_finalize(l3_ctx* ctx);
 /* Zero every KV cache (the reference never does this; provided for reuse). */
 int l3_reset_cache(l3_ctx* ctx);
@@ -118,7 +120,9 @@ int l3_layer_forward_host(l3_ctx* ctx, int32_t layer, const float* x_host, int32
 
 /* ---- one attention (replaces Attention.__call__, llama3.py:155-213) ------ */
 /* x [B, L, D] = the already-normalised block input; out [B, L, D] = O-projection
- * output without residual.  Uses and updates the layer's KV cache. */
+ * output without residual.  Uses and updates the layer's KV cache.  Needs a
+ * context whose layer holds only attention weights (no attention norm: a
+ * folded layer is refused). */
 int l3_attention_forward_host(l3_ctx* ctx, int32_t layer, const float* x_host, int32_t B,
                               int32_t L, int32_t start_pos, float* out_host);
 

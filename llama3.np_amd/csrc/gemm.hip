@@ -4,12 +4,14 @@
 
 namespace l3 {
 
+// Product kernels use the register-direct epilogue (DIRECT): RMSNorm weights are folded into W
+// at l3_finalize, the row factor comes from the A fragments, the tile leaves from registers.
 template <int EPI, int WM, int WN, int TM, int TN, int WPE, int BK = 32>
 static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK>), dim3((unsigned)tiles),
-                       dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>),
+                       dim3((unsigned)tiles), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
@@ -31,6 +33,7 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.K % 32 != 0 || a.K <= 0) return hipErrorInvalidValue;  // whole 32-deep k-tiles
     if (epi == EPI_SWIGLU && a.N % 32 != 0) return hipErrorInvalidValue;
     if (a.N % 4 != 0 || a.ldc % 4 != 0 || a.lda % 4 != 0) return hipErrorInvalidValue;  // 16-B rows
+    if (a.norm_w) return hipErrorInvalidValue;  // norm weights are folded into W (l3_finalize)
     // M <= 8 (decode, short prompts): weight-streaming GEMV with the same epilogues
     const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
     if (a.M <= 8 && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS
@@ -43,26 +46,24 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         }
     }
     // Configurations chosen with tools/gemm_tune (interleaved A/B on MI355X).
+    // BK 16 kernels use the swizzled unpadded LDS image (32 KB at 128 x 128 -> 3 blocks/CU).
     const bool small_m = a.M <= 32;  // tiny M: 16 x 128 tile
     switch (epi) {
-        case EPI_SWIGLU:  // 128 x 128, BK 16: 142 VGPRs + 48 KB LDS -> 3 blocks per CU
+        case EPI_SWIGLU:  // 128 x 128, BK 16
             if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2>(a, s);
-            return launch<EPI_SWIGLU, 2, 2, 4, 4, 2, 16>(a, s);
-        case EPI_QKV:     // N = 864 (stories15M) / 6144 (Llama-3 shape) are multiples of 96
+            return launch<EPI_SWIGLU, 2, 2, 4, 4, 3, 16>(a, s);
+        case EPI_QKV:     // 128 x 128, BK 16 (tiles may straddle the q|k|v sections: per-float4)
             if (small_m) return launch<EPI_QKV, 1, 4, 1, 2, 2>(a, s);
-            if (a.N % 96 == 0)
-                return a.K <= 1024 ? launch<EPI_QKV, 2, 2, 2, 3, 3, 16>(a, s)   // 64 x 96
-                                   : launch<EPI_QKV, 2, 2, 4, 3, 3, 16>(a, s);  // 128 x 96
-            return launch<EPI_QKV, 2, 2, 2, 4, 3, 16>(a, s);                    // 64 x 128
+            return launch<EPI_QKV, 2, 2, 4, 4, 3, 16>(a, s);
         case EPI_RESID:   // O-proj / down
             if (small_m) return launch<EPI_RESID, 1, 4, 1, 2, 2>(a, s);
             if (a.N % 96 == 0)
                 return a.K <= 512 ? launch<EPI_RESID, 2, 2, 2, 3, 2>(a, s)   // 64 x 96
                                   : launch<EPI_RESID, 2, 2, 4, 3, 2>(a, s);  // 128 x 96
-            return launch<EPI_RESID, 2, 2, 4, 4, 2, 16>(a, s);               // 128 x 128
+            return launch<EPI_RESID, 2, 2, 4, 4, 3, 16>(a, s);               // 128 x 128
         case EPI_STORE:   // lm_head, op-level linear
             if (small_m) return launch<EPI_STORE, 1, 4, 1, 2, 2>(a, s);
-            return launch<EPI_STORE, 2, 2, 4, 4, 2>(a, s);
+            return launch<EPI_STORE, 2, 2, 4, 4, 3, 16>(a, s);
         default:
             return hipErrorInvalidValue;
     }

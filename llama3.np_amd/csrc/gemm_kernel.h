@@ -163,6 +163,75 @@ __device__ __forceinline__ void store_tile(const GemmArgs& p, const float* stage
     }
 }
 
+// Register-direct epilogue (DIRECT kernels).  The MFMA operands are swapped (W fragment as
+// the A operand, activation fragment as B), so the accumulator of tile (i, j) is C^T: lane l
+// holds C[row = 16i + (l&15)][col = 16j + 4(l>>4) + r], r = 0..3 — four consecutive columns
+// of one row, i.e. one 16-byte store, with no LDS staging and no block barrier.  rs[i] is the
+// lane's RMSNorm factor for its row of tile i (1 without norm); res the prefetched residual.
+template <int TM, int TN, int EPI, int NR>
+__device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (&acc)[TM][TN],
+                                                const float (&rs)[TM], const f32x4 (&res)[NR],
+                                                int mrow0, int ncol0, int lane) {
+    const int frow = lane & 15, fq4 = 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int row = mrow0 + i * 16 + frow;
+        if (row >= p.M) continue;
+        const float sc = rs[i];
+        if constexpr (EPI == EPI_SWIGLU) {
+            // fused W rows in 16-row groups: tile j (even) = gate, j + 1 = up of the same
+            // 16 hidden units (ncol0 + 16j is a multiple of 32)
+#pragma unroll
+            for (int j = 0; j < TN; j += 2) {
+                const int hcol = (ncol0 + j * 16) / 2 + fq4;
+                if (hcol >= p.N / 2) continue;
+                const f32x4 g = acc[i][j] * sc, u = acc[i][j + 1] * sc;
+                const f32x4 v = {silu_f(g.x) * u.x, silu_f(g.y) * u.y, silu_f(g.z) * u.z, silu_f(g.w) * u.w};
+                *reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + hcol) = v;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = ncol0 + j * 16 + fq4;
+                if (col >= p.N) continue;
+                f32x4 v = acc[i][j];
+                if constexpr (EPI == EPI_QKV) {
+                    v *= sc;
+                    // RoPE on the two (even, odd) pairs of the float4 (llama3.py:41-76), then
+                    // q scaling / KV-cache append (llama3.py:184-185)
+                    const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
+                    const int bidx = row / p.L, pos = start_of(p) + row - bidx * p.L;
+                    const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
+                    const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
+                    const int head = cc / p.HD, d = cc - head * p.HD;
+                    if (is_q || is_k) {
+                        const int t = pos * (p.HD >> 1) + (d >> 1);
+                        const float2 c = *reinterpret_cast<const float2*>(p.rope_cos + t);
+                        const float2 sn = *reinterpret_cast<const float2*>(p.rope_sin + t);
+                        v = f32x4{v.x * c.x - v.y * sn.x, v.x * sn.x + v.y * c.x,
+                                  v.z * c.y - v.w * sn.y, v.z * sn.y + v.w * c.y};
+                    }
+                    if (is_q) {
+                        *reinterpret_cast<f32x4*>(p.q_out + (int64_t)row * qdim + col) = v * p.q_scale;
+                    } else {
+                        float* cache = is_k ? p.cache_k : p.cache_v;
+                        *reinterpret_cast<f32x4*>(cache + (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d) = v;
+                    }
+                } else {
+                    float* dst = p.C + (int64_t)row * p.ldc + col;
+                    if constexpr (EPI == EPI_RESID) {
+                        if constexpr (NR == TM * TN) v += res[i * TN + j];
+                        else v += *reinterpret_cast<const f32x4*>(dst);
+                    } else {
+                        v *= sc;
+                    }
+                    *reinterpret_cast<f32x4*>(dst) = v;
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // LDS-staged main loop
 
@@ -176,11 +245,17 @@ __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
 }
 
 template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false,
-          int BK = 32>
+          int BK = 32, bool DIRECT = false>
 __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
     constexpr int BM = WM * TM * 16;
     constexpr int BN = WN * TN * 16;
-    constexpr int LDS_STRIDE = BK + 8;  // == 8 mod 16 floats for BK in {16, 32, 64}
+    // LDS image rows: BK >= 32 -> padded stride BK + 8 (== 8 mod 16 floats: conflict-free
+    // ds_read_b128, and an 8-lane ds_write_b128 group writes one whole row).  BK = 16 -> no
+    // padding, float4 quad q of row r stored at quad q ^ ((r >> 1) & 3): the 8-lane write
+    // groups (two rows) and the 16-lane read groups (16 rows, one quad) both land on distinct
+    // banks (checked against the MI355X_MICROARCH.md lane groups), and the image is 1/3 smaller
+    constexpr bool SWZ = BK == 16;
+    constexpr int LDS_STRIDE = SWZ ? 16 : BK + 8;
     constexpr int Q = BK / 4;           // float4 per staged row
     static_assert(BK % 16 == 0 && (Q & (Q - 1)) == 0, "BK must be 16, 32 or 64");
     constexpr int A_F4 = BM * BK / 4;
@@ -191,7 +266,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     // one LDS array: [2][BM][stride] A image, then [2][BN][stride] B image; after the main
     // loop its head holds the per-row RMSNorm factors, then the staged output tile
     constexpr int MAIN_F = 2 * (BM + BN) * LDS_STRIDE;
-    constexpr int EPI_F = ((BM + 3) & ~3) + BM * OutTile<BM, BN, EPI>::STRIDE;
+    constexpr int EPI_F = DIRECT ? 0 : ((BM + 3) & ~3) + BM * OutTile<BM, BN, EPI>::STRIDE;
     __shared__ __attribute__((aligned(16))) float smem[MAIN_F > EPI_F ? MAIN_F : EPI_F];
     float (*As)[BM][LDS_STRIDE] = reinterpret_cast<float (*)[BM][LDS_STRIDE]>(smem);
     float (*Bs)[BN][LDS_STRIDE] = reinterpret_cast<float (*)[BN][LDS_STRIDE]>(smem + 2 * BM * LDS_STRIDE);
@@ -202,7 +277,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     const int ntn = (p.N + BN - 1) / BN;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
-    unsigned long long stamps[6];
+    unsigned long long stamps[12];
     if constexpr (STAMP) {
         __builtin_amdgcn_sched_barrier(0);
         stamp_pair(stamps);
@@ -210,9 +285,12 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     }
 
     f32x4 ra[A_IT], rb[B_IT];
-    float ss[A_IT];
+    // RMSNorm sums of squares: per staged A row (LDS epilogue) or, DIRECT, per lane from its
+    // own A fragments (row 16i + (lane&15) of the wave tile, a quarter of K per lane)
+    constexpr int NSS = DIRECT ? TM : A_IT;
+    float ss[NSS];
 #pragma unroll
-    for (int i = 0; i < A_IT; ++i) ss[i] = 0.f;
+    for (int i = 0; i < NSS; ++i) ss[i] = 0.f;
 
     auto gload = [&](int k0) {
 #pragma unroll
@@ -238,24 +316,27 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     };
     auto sstore = [&](int buf, int k0) {
         f32x4 wv = {1.f, 1.f, 1.f, 1.f};
-        if (p.norm) wv = *reinterpret_cast<const f32x4*>(p.norm_w + k0 + (tid % Q) * 4);
+        if (!DIRECT && p.norm) wv = *reinterpret_cast<const f32x4*>(p.norm_w + k0 + (tid % Q) * 4);
 #pragma unroll
         for (int i = 0; i < A_IT; ++i) {
             const int f = tid + 256 * i;  // f % Q == tid % Q: one norm-weight quad per thread
             if (A_F4 % 256 == 0 || f < A_F4) {
                 f32x4 v = ra[i];
-                if (p.norm) {
+                if (!DIRECT && p.norm) {
                     ss[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
                     v *= wv;
                 }
-                *reinterpret_cast<f32x4*>(&As[buf][f / Q][(f % Q) * 4]) = v;
+                const int r = f / Q, q = f % Q;
+                *reinterpret_cast<f32x4*>(&As[buf][r][(SWZ ? q ^ ((r >> 1) & 3) : q) * 4]) = v;
             }
         }
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
             const int f = tid + 256 * i;
-            if (B_F4 % 256 == 0 || f < B_F4)
-                *reinterpret_cast<f32x4*>(&Bs[buf][f / Q][(f % Q) * 4]) = rb[i];
+            if (B_F4 % 256 == 0 || f < B_F4) {
+                const int r = f / Q, q = f % Q;
+                *reinterpret_cast<f32x4*>(&Bs[buf][r][(SWZ ? q ^ ((r >> 1) & 3) : q) * 4]) = rb[i];
+            }
         }
     };
 
@@ -267,6 +348,8 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 
     const int frow = lane & 15, fk = 4 * (lane >> 4);
     const int arow0 = wm * TM * 16, brow0 = wn * TN * 16;
+    // fragment column in the image: rows 16i + frow share (frow >> 1) & 3 for the swizzle
+    const int fcol = SWZ ? 4 * ((lane >> 4) ^ ((frow >> 1) & 3)) : fk;
 
     auto compute = [&](int buf) {
 #pragma unroll
@@ -274,25 +357,42 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             f32x4 a[TM], bw[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(&As[buf][arow0 + i * 16 + frow][kg * 16 + fk]);
+                a[i] = *reinterpret_cast<const f32x4*>(&As[buf][arow0 + i * 16 + frow][kg * 16 + fcol]);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                bw[j] = *reinterpret_cast<const f32x4*>(&Bs[buf][brow0 + j * 16 + frow][kg * 16 + fk]);
+                bw[j] = *reinterpret_cast<const f32x4*>(&Bs[buf][brow0 + j * 16 + frow][kg * 16 + fcol]);
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma4(a[i][s], bw[j][s], acc[i][j]);
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = DIRECT ? mfma4(bw[j][s], a[i][s], acc[i][j])
+                                           : mfma4(a[i][s], bw[j][s], acc[i][j]);
+            if constexpr (DIRECT) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+                    ss[i] += a[i].x * a[i].x + a[i].y * a[i].y + a[i].z * a[i].z + a[i].w * a[i].w;
+            }
         }
     };
 
-    f32x4 res[OutTile<BM, BN, EPI>::RES_PREFETCH ? OutTile<BM, BN, EPI>::IT : 1];
+    // residual prefetch (EPI_RESID): LDS epilogue -> its row-major float4 map; DIRECT -> the
+    // lane's own (row, 4 columns) of every accumulator tile, when at most 12 float4
+    constexpr bool DIRECT_RES = DIRECT && EPI == EPI_RESID && TM * TN <= 12;
+    constexpr int NRES = DIRECT ? (DIRECT_RES ? TM * TN : 1)
+                                : (OutTile<BM, BN, EPI>::RES_PREFETCH ? OutTile<BM, BN, EPI>::IT : 1);
+    f32x4 res[NRES];
 
     const int nk = p.K / BK;
     gload(0);
     sstore(0, 0);
     __syncthreads();
+    if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        stamp_pair(stamps + 2);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     for (int kt = 0; kt < nk - 1; ++kt) {
         const int cur = kt & 1;
         gload((kt + 1) * BK);
@@ -302,9 +402,52 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     }
     // last k-tile, peeled: its staging registers are dead, so the residual tile of EPI_RESID is
     // fetched here and its latency hides behind this tile's MFMAs
-    if constexpr (EPI == EPI_RESID && OutTile<BM, BN, EPI>::RES_PREFETCH)
+    if constexpr (DIRECT_RES) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int row = m0 + arow0 + i * 16 + frow, col = n0 + brow0 + j * 16 + fk;
+                res[i * TN + j] = (row < p.M && col < p.N)
+                                      ? *reinterpret_cast<const f32x4*>(p.C + (int64_t)row * p.ldc + col)
+                                      : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+    } else if constexpr (!DIRECT && EPI == EPI_RESID && OutTile<BM, BN, EPI>::RES_PREFETCH) {
         load_residual<BM, BN, EPI>(p, res, m0, n0, tid);
+    }
     compute((nk - 1) & 1);
+
+    if constexpr (DIRECT) {
+        // no barrier: each wave finishes its own tile from registers
+        float rs[TM];
+        const float inv_k = 1.0f / (float)p.K;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            float v = ss[i];
+            v += __shfl_xor(v, 16);  // the four k-quarters of the row
+            v += __shfl_xor(v, 32);
+            rs[i] = p.norm ? 1.0f / sqrtf(v * inv_k + p.eps) : 1.0f;
+        }
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            stamp_pair(stamps + 4);
+            stamp_pair(stamps + 6);
+            stamp_pair(stamps + 8);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        direct_epilogue<TM, TN, EPI>(p, acc, rs, res, m0 + arow0, n0 + brow0, lane);
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            stamp_pair(stamps + 10);
+            if (tid == 0) {
+                unsigned long long* d = p.stamps + (size_t)blockIdx.x * 14;
+                for (int i = 0; i < 12; ++i) d[i] = stamps[i];
+                d[12] = 0;
+                d[13] = t;
+            }
+        }
+        return;
+    }
     __syncthreads();
 
     if (p.norm) {
@@ -323,7 +466,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     const bool nrm = p.norm;
     if constexpr (STAMP) {
         __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps + 2);
+        stamp_pair(stamps + 4);
         __builtin_amdgcn_sched_barrier(0);
     }
     // staged epilogue: the tile goes after the row factors in the (idle) LDS array
@@ -335,18 +478,28 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         for (int r = 0; r < 4; ++r) sc_reg[i][r] = nrm ? row_scale[arow0 + i * 16 + fk + r] : 1.0f;
     stage_tile<BM, BN, TM, TN, EPI>(p, acc, stage, m0, n0, arow0, brow0, lane,
                                     [&](int i, int r) { return sc_reg[i][r]; });
+    if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        stamp_pair(stamps + 6);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     __syncthreads();
+    if constexpr (STAMP) {
+        __builtin_amdgcn_sched_barrier(0);
+        stamp_pair(stamps + 8);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     store_tile<BM, BN, EPI>(p, stage, res, m0, n0, tid);
     if constexpr (STAMP) {
         __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps + 4);
+        stamp_pair(stamps + 10);
         if (tid == 0) {
-            unsigned long long* d = p.stamps + (size_t)blockIdx.x * 8;
-            for (int i = 0; i < 6; ++i) d[i] = stamps[i];
+            unsigned long long* d = p.stamps + (size_t)blockIdx.x * 14;
+            for (int i = 0; i < 12; ++i) d[i] = stamps[i];
             unsigned xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            d[6] = xcc;
-            d[7] = t;
+            d[12] = xcc;
+            d[13] = t;
         }
     }
 }
@@ -373,7 +526,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
         f32x4 v = *reinterpret_cast<const f32x4*>(p.A + (int64_t)m * p.lda + k);
         if (p.norm) {
             atomicAdd(&rsum[m], v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
-            v *= *reinterpret_cast<const f32x4*>(p.norm_w + k);
+            // the norm weight itself is folded into W (launch_fold_cols)
         }
         *reinterpret_cast<f32x4*>(xs + m * p.K + k) = v;
     }

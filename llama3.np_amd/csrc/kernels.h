@@ -18,8 +18,10 @@ struct GemmArgs {
     const float* W;                // [N, K] row-major
     float* C; int64_t ldc;         // output (EPI_QKV: unused)
     int M, N, K;
-    bool norm;                     // RMSNorm on A: A*norm_w, rows scaled by 1/sqrt(mean(A^2)+eps)
-    const float* norm_w;           // [K] (when norm)
+    bool norm;                     // RMSNorm on A: rows scaled by 1/sqrt(mean(A^2)+eps); the norm
+                                   // weight is folded into W's columns (launch_fold_cols)
+    const float* norm_w;           // must be null for launch_gemm (folded); the LDS-epilogue
+                                   // kernels in tools/gemm_tune still multiply A by it
     float eps;
     // EPI_QKV
     float* q_out;                  // [M, H*HD], pre-scaled by q_scale
@@ -28,7 +30,7 @@ struct GemmArgs {
     int L, start_pos, H, KVH, HD, Smax;
     const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
-    unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 8 per block
+    unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 14 per block
 };
 
 struct AttnArgs {
@@ -56,6 +58,7 @@ hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStre
 hipError_t launch_silu(const float* x, float* y, int64_t n, hipStream_t s);
 hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows, int dim,
                           float eps, hipStream_t s);
+hipError_t launch_fold_cols(float* W, int64_t rows, int K, const float* w, hipStream_t s);
 hipError_t launch_rope(const float* x, float* y, const float* cos_t, const float* sin_t, int B,
                        int L, int nh, int hd, hipStream_t s);
 

@@ -172,4 +172,23 @@ hipError_t launch_rope(const float* x, float* y, const float* cos_t, const float
     return hipGetLastError();
 }
 
+// W[r][k] *= w[k]: folds an RMSNorm weight into the K columns of the matrix that consumes the
+// normalised activations (rmsnorm(x) @ W^T = diag(1/rms(x)) * x @ (W * w)^T), once at
+// l3_finalize.  HBM-bound, float4 per thread.
+__global__ void fold_cols_kernel(float* W, int64_t n4, int K4, const float* w) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n4) return;
+    f32x4 v = reinterpret_cast<f32x4*>(W)[i];
+    v *= reinterpret_cast<const f32x4*>(w)[i % K4];
+    reinterpret_cast<f32x4*>(W)[i] = v;
+}
+
+hipError_t launch_fold_cols(float* W, int64_t rows, int K, const float* w, hipStream_t s) {
+    if (K % 4) return hipErrorInvalidValue;
+    const int64_t n4 = rows * (K / 4);
+    if (n4 == 0) return hipSuccess;
+    hipLaunchKernelGGL(fold_cols_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, W, n4, K / 4, w);
+    return hipGetLastError();
+}
+
 }  // namespace l3

@@ -68,6 +68,8 @@ struct Layer {
     float* cache_k = nullptr;
     float* cache_v = nullptr;
     unsigned have = 0;  // bitmask of uploaded kinds
+    // RMSNorm weight folded into the consuming GEMM's W columns at l3_finalize
+    bool folded_qkv = false, folded_gu = false;
 };
 
 struct Timer {
@@ -87,6 +89,7 @@ struct l3_ctx {
     float* rope_sin = nullptr;
     std::vector<Layer> layers;
     bool have_emb = false, have_lm = false, have_fnorm = false, finalized = false;
+    bool folded_lm = false;
     // workspace
     int64_t ws_T = 0, ws_B = 0;
     float *h = nullptr, *q = nullptr, *attn = nullptr, *hid = nullptr, *logits = nullptr;
@@ -193,7 +196,7 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 2;  // bumped whenever a hot kernel changes (keys profiles/pmc_*.json)
+    if (minor) *minor = 3;  // bumped whenever a hot kernel changes (keys profiles/pmc_*.json)
     return 0;
 }
 
@@ -369,15 +372,40 @@ static const unsigned NEED_LAYER = NEED_ATTN | (1u << L3_W_GATE) | (1u << L3_W_U
 
 extern "C" int l3_finalize(l3_ctx* c) {
     CHECK_CTX(c);
+    if (c->finalized) return 0;
     if (set_dev(c)) return 1;
-    HIP_TRY(hipDeviceSynchronize());  // uploads were synchronous; keep the contract explicit
+    // Fold each RMSNorm weight into the columns of the GEMM that consumes the normalised rows
+    // (attention norm -> wqkv, FFN norm -> wgu, final norm -> lm_head): the GEMMs then apply
+    // only the per-row 1/rms factor.  Only where both were uploaded: a layer-only (attention)
+    // context keeps its raw projections.
+    const int D = c->d.dim;
+    const unsigned QKV = (1u << L3_W_Q) | (1u << L3_W_K) | (1u << L3_W_V);
+    const unsigned GU = (1u << L3_W_GATE) | (1u << L3_W_UP);
+    for (auto& L : c->layers) {
+        if ((L.have & QKV) == QKV && (L.have & (1u << L3_W_ATTN_NORM))) {
+            HIP_TRY(launch_fold_cols(L.wqkv, c->qkvn, D, L.n_attn, c->stream));
+            L.folded_qkv = true;
+        }
+        if ((L.have & GU) == GU && (L.have & (1u << L3_W_FFN_NORM))) {
+            HIP_TRY(launch_fold_cols(L.wgu, 2 * (int64_t)c->d.hidden_dim, D, L.n_ffn, c->stream));
+            L.folded_gu = true;
+        }
+    }
+    if (c->have_lm && c->have_fnorm) {
+        HIP_TRY(launch_fold_cols(c->lm_head, c->d.vocab_size, D, c->final_norm, c->stream));
+        c->folded_lm = true;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
     c->finalized = true;
     return 0;
 }
 
 static int need_layer(l3_ctx* c, int li, unsigned mask) {
-    if ((c->layers[li].have & mask) != mask)
-        return fail("layer %d is missing weights (have 0x%x, need 0x%x)", li, c->layers[li].have, mask);
+    const Layer& L = c->layers[li];
+    if ((L.have & mask) != mask)
+        return fail("layer %d is missing weights (have 0x%x, need 0x%x)", li, L.have, mask);
+    if (mask == NEED_LAYER && !(L.folded_qkv && L.folded_gu))
+        return fail("layer %d: norm weights not folded (l3_finalize before any forward)", li);
     return 0;
 }
 
@@ -425,7 +453,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     g.eps = c->d.norm_eps;
     // rmsnorm -> QKV -> RoPE -> q + KV-cache append
     g.A = c->h; g.lda = D; g.W = Ly.wqkv; g.C = nullptr; g.ldc = 0;
-    g.M = (int)T; g.N = c->qkvn; g.K = D; g.norm = true; g.norm_w = Ly.n_attn;
+    g.M = (int)T; g.N = c->qkvn; g.K = D; g.norm = true;  // n_attn folded into wqkv
     g.q_out = c->q; g.cache_k = Ly.cache_k; g.cache_v = Ly.cache_v;
     g.rope_cos = c->rope_cos; g.rope_sin = c->rope_sin;
     g.L = L; g.start_pos = start_pos; g.H = c->d.n_heads; g.KVH = c->d.n_kv_heads; g.HD = c->HD;
@@ -447,7 +475,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     // rmsnorm -> gate|up -> SwiGLU
     GemmArgs gu{};
     gu.A = c->h; gu.lda = D; gu.W = Ly.wgu; gu.C = c->hid; gu.ldc = FD;
-    gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true; gu.norm_w = Ly.n_ffn;
+    gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true;  // n_ffn folded into wgu
     gu.eps = c->d.norm_eps;
     if (timed(c, L3_K_GATEUP, [&] { return launch_gemm(EPI_SWIGLU, gu, c->stream); })) return 1;
     // down + residual
@@ -470,7 +498,7 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
     GemmArgs lm{};
     lm.A = c->h + (int64_t)(L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
     lm.C = logits_dev; lm.ldc = c->d.vocab_size;
-    lm.M = B; lm.N = c->d.vocab_size; lm.K = D; lm.norm = true; lm.norm_w = c->final_norm;
+    lm.M = B; lm.N = c->d.vocab_size; lm.K = D; lm.norm = true;  // final norm folded
     lm.eps = c->d.norm_eps;
     if (timed(c, L3_K_LMHEAD, [&] { return launch_gemm(EPI_STORE, lm, c->stream); })) return 1;
     return 0;
@@ -654,6 +682,9 @@ extern "C" int l3_attention_forward_host(l3_ctx* c, int32_t layer, const float* 
         ensure_ws(c, B, L))
         return 1;
     Layer& Ly = c->layers[layer];
+    if (Ly.folded_qkv)  // this layer's wqkv carries its attention norm (full-layer context)
+        return fail("l3_attention_forward: layer %d has the attention norm folded into its "
+                    "projections; use a context holding only the attention weights", layer);
     const int64_t T = (int64_t)B * L;
     const int D = c->d.dim;
     HIP_TRY(hipMemcpyAsync(c->h, x_host, T * D * 4, hipMemcpyHostToDevice, c->stream));

@@ -27,6 +27,7 @@ using namespace l3;
 struct Variant {
     std::string name;
     std::function<void(const GemmArgs&, hipStream_t)> run;
+    bool direct = false;  // register-direct epilogue: takes W with the norm weight folded in
 };
 
 
@@ -43,6 +44,13 @@ struct Variant {
                 const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
                 hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
             }}
+
+#define DVAR(WM, WN, TM, TN, EPI, WPE, BK)                                                            \
+    Variant{"direct<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
+                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
+                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
+                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
+            }, true}
 
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
@@ -82,6 +90,20 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
         g.C = qo;  // the correctness check reads the q section
         g.ldc = 288;
     }
+    // direct variants: W with the RMSNorm weight folded into its columns (as the runtime does)
+    float* Wf = W;
+    if (norm) {
+        std::vector<float> hWf(hW);
+        for (size_t n = 0; n < (size_t)N; ++n)
+            for (size_t k = 0; k < (size_t)K; ++k) hWf[n * K + k] *= hw[k];
+        CK(hipMalloc(&Wf, hWf.size() * 4));
+        CK(hipMemcpy(Wf, hWf.data(), hWf.size() * 4, hipMemcpyHostToDevice));
+    }
+    auto args_for = [&](const Variant& v) {
+        GemmArgs a = g;
+        if (v.direct) a.W = Wf;
+        return a;
+    };
     hipStream_t s;
     CK(hipStreamCreate(&s));
     const double flops = 2.0 * M * N * K;
@@ -91,7 +113,7 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
     std::vector<float> ref((size_t)M * outN), got((size_t)M * outN);
     for (size_t v = 0; v < vars.size(); ++v) {
         CK(hipMemsetAsync(g.C, 0, (size_t)M * outN * 4, s));
-        vars[v].run(g, s);
+        vars[v].run(args_for(vars[v]), s);
         CK(hipGetLastError());
         CK(hipStreamSynchronize(s));
         CK(hipMemcpy(v ? got.data() : ref.data(), g.C, got.size() * 4, hipMemcpyDeviceToHost));
@@ -111,8 +133,9 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
     CK(hipEventCreate(&e1));
     for (int r = 0; r < rounds + 1; ++r) {
         for (size_t v = 0; v < vars.size(); ++v) {
+            const GemmArgs a = args_for(vars[v]);
             CK(hipEventRecord(e0, s));
-            for (int i = 0; i < iters; ++i) vars[v].run(g, s);
+            for (int i = 0; i < iters; ++i) vars[v].run(a, s);
             CK(hipEventRecord(e1, s));
             CK(hipEventSynchronize(e1));
             float ms = 0;
@@ -128,12 +151,16 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
                vars[v].name.c_str(), med, med / 157.3 * 100, x.front(), x.back(), flops / (med * 1e12) * 1e6);
     }
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(w)); CK(hipFree(C));
+    if (Wf != W) CK(hipFree(Wf));
     if (qo) { CK(hipFree(qo)); CK(hipFree(ck)); CK(hipFree(cv)); CK(hipFree(rc)); CK(hipFree(rsn)); }
     CK(hipStreamDestroy(s));
 }
 
 // Diagnostic: clock and cycle split per block from in-kernel stamps (STAMP build).
-template <int WM, int WN, int TM, int TN, int EPI>
+// Per block: shader-clock (s_memtime) and 100 MHz real-time stamps at start, after the first
+// k-tile is staged (prologue), after the main loop, and at the end (epilogue).  Residency =
+// sum of block lifetimes / (launch span x 256 CUs): the average number of blocks a CU holds.
+template <int WM, int WN, int TM, int TN, int EPI, int WPE, int BK>
 static void stamp_report(const char* label, int M, int K, int N, bool norm) {
     const int outN = EPI == EPI_SWIGLU ? N / 2 : N;
     float *A, *W, *w, *C;
@@ -147,37 +174,48 @@ static void stamp_report(const char* label, int M, int K, int N, bool norm) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     unsigned long long* st;
-    CK(hipMalloc(&st, (size_t)tiles * 8 * 8));
+    CK(hipMalloc(&st, (size_t)tiles * 14 * 8));
     GemmArgs g{};
     g.A = A; g.lda = K; g.W = W; g.C = C; g.ldc = outN; g.M = M; g.N = N; g.K = K;
     g.norm = norm; g.norm_w = w; g.eps = 1e-6f; g.stamps = st;
-    for (int it = 0; it < 20; ++it)  // >= 2 s of back-to-back launches is the guide's rule for
-        hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, 2, true>), dim3(tiles), dim3(256), 0, 0, g);
+    for (int it = 0; it < 20; ++it)  // back-to-back launches so the clock settles; last one kept
+        hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, true, BK>), dim3(tiles), dim3(256), 0, 0, g);
     CK(hipDeviceSynchronize());
-    std::vector<unsigned long long> h((size_t)tiles * 8);
+    std::vector<unsigned long long> h((size_t)tiles * 14);
     CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-    std::vector<double> mhz, loop, epi;
+    std::vector<double> mhz, pro, loop, epi, e_stage, e_bar, e_store;
     unsigned long long t0 = ~0ull, t1 = 0;
+    double life = 0;
     for (int b = 0; b < tiles; ++b) {
-        const unsigned long long* d = &h[(size_t)b * 8];
-        if (d[3] > d[1]) mhz.push_back((double)(d[4] - d[0]) / (double)(d[5] - d[1]) * 100.0);
-        loop.push_back((double)(d[2] - d[0]));
-        epi.push_back((double)(d[4] - d[2]));
-        t0 = std::min(t0, d[1]); t1 = std::max(t1, d[5]);
+        const unsigned long long* d = &h[(size_t)b * 14];
+        if (d[11] > d[1]) mhz.push_back((double)(d[10] - d[0]) / (double)(d[11] - d[1]) * 100.0);
+        pro.push_back((double)(d[2] - d[0]));
+        loop.push_back((double)(d[4] - d[2]));
+        epi.push_back((double)(d[10] - d[4]));
+        e_stage.push_back((double)(d[6] - d[4]));
+        e_bar.push_back((double)(d[8] - d[6]));
+        e_store.push_back((double)(d[10] - d[8]));
+        life += (double)(d[11] - d[1]);
+        t0 = std::min(t0, d[1]); t1 = std::max(t1, d[11]);
     }
     auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
     const double mfma_cycles = (double)K / 4 * TM * TN * 32;  // per wave, 16x16x4 f32 at 32 cyc
-    printf("\n== stamps %s: blocks %d, clock median %.0f MHz, main loop median %.0f cyc (MFMA-only "
-           "%.0f cyc per wave), epilogue median %.0f cyc, last launch span %.1f us\n",
-           label, tiles, med(mhz), med(loop), mfma_cycles, med(epi), (t1 - t0) / 100.0);
+    const double span = (double)(t1 - t0);
+    printf("\n== stamps %s wpe%d bk%d: blocks %d, clock median %.0f MHz, prologue median %.0f cyc, "
+           "main loop median %.0f cyc (MFMA-only %.0f cyc per wave), epilogue median %.0f cyc, "
+           "launch span %.1f us, residency %.2f blocks/CU\n"
+           "   epilogue split (wave 0): stage %.0f, barrier %.0f, store %.0f cyc\n",
+           label, WPE, BK, tiles, med(mhz), med(pro), med(loop), mfma_cycles, med(epi), span / 100.0,
+           life / (span * 256.0), med(e_stage), med(e_bar), med(e_store));
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(w)); CK(hipFree(C)); CK(hipFree(st));
 }
 
 int main(int argc, char** argv) {
     if (argc > 3 && std::string(argv[3]) == "stamps") {
-        stamp_report<2, 2, 4, 4, EPI_SWIGLU>("gate|up 128x128", 65536, 288, 1536, true);
-        stamp_report<2, 2, 4, 3, EPI_RESID>("down 128x96", 65536, 768, 288, false);
-        stamp_report<2, 2, 4, 3, EPI_RESID>("O-proj 128x96", 65536, 288, 288, false);
+        stamp_report<2, 2, 4, 4, EPI_SWIGLU, 2, 16>("gate|up 128x128", 65536, 288, 1536, true);
+        stamp_report<2, 2, 4, 4, EPI_SWIGLU, 3, 16>("gate|up 128x128", 65536, 288, 1536, true);
+        stamp_report<2, 2, 4, 3, EPI_RESID, 2, 32>("down 128x96", 65536, 768, 288, false);
+        stamp_report<2, 2, 2, 3, EPI_RESID, 2, 32>("O-proj 64x96", 65536, 288, 288, false);
         return 0;
     }
     const int rounds = argc > 1 ? atoi(argv[1]) : 5;
@@ -186,13 +224,17 @@ int main(int argc, char** argv) {
     const bool c5 = argc > 3 && std::string(argv[3]) == "c5";
     if (!c5) {
     run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
-              {BVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 16), BVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16)}, rounds, iters);
+              {BVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), DVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
+               DVAR(2, 2, 4, 4, EPI_SWIGLU, 4, 16), DVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, iters);
     run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
-              {BVAR(2, 2, 2, 3, EPI_QKV, 3, 16), BVAR(2, 2, 2, 3, EPI_QKV, 4, 16)}, rounds, iters);
+              {BVAR(2, 2, 2, 3, EPI_QKV, 3, 16), DVAR(2, 2, 2, 3, EPI_QKV, 3, 16),
+               DVAR(2, 2, 4, 3, EPI_QKV, 3, 16), DVAR(2, 2, 4, 4, EPI_QKV, 3, 16)}, rounds, iters);
     run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
-              {BVAR(2, 2, 4, 3, EPI_RESID, 2, 32)}, rounds, iters);
+              {BVAR(2, 2, 4, 3, EPI_RESID, 2, 32), DVAR(2, 2, 4, 3, EPI_RESID, 2, 32),
+               DVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
     run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
-              {BVAR(2, 2, 2, 3, EPI_RESID, 2, 32)}, rounds, iters);
+              {BVAR(2, 2, 2, 3, EPI_RESID, 2, 32), DVAR(2, 2, 2, 3, EPI_RESID, 2, 32),
+               DVAR(2, 2, 2, 3, EPI_RESID, 3, 16), DVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
     } else {
     // Llama-3-8B shapes (C5) at M = 16384 rows (tuning size)
     const int Mc = 16384;
