@@ -4,13 +4,14 @@
 
 namespace l3 {
 
-// Product kernels use the register-direct epilogue (DIRECT): RMSNorm weights are folded into W
-// at l3_finalize, the row factor comes from the A fragments, the tile leaves from registers.
-template <int EPI, int WM, int WN, int TM, int TN, int WPE, int BK = 32>
+// Product kernels: k-tiles filled by global_load_lds (GLDS) and the register-direct epilogue
+// (DIRECT): RMSNorm weights are folded into W at l3_finalize, the row factor comes from the A
+// fragments, the tile leaves from registers.
+template <int EPI, int WM, int WN, int TM, int TN, int WPE, int BK>
 static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>),
+    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, true>),
                        dim3((unsigned)tiles), dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -46,23 +47,24 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         }
     }
     // Configurations chosen with tools/gemm_tune (interleaved A/B on MI355X).
-    // BK 16 kernels use the swizzled unpadded LDS image (32 KB at 128 x 128 -> 3 blocks/CU).
+    // 128 x 128 BK16: 120 VGPRs + 32 KB LDS -> 4 blocks per CU.
     const bool small_m = a.M <= 32;  // tiny M: 16 x 128 tile
     switch (epi) {
         case EPI_SWIGLU:  // 128 x 128, BK 16
-            if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2>(a, s);
+            if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2, 32>(a, s);
             return launch<EPI_SWIGLU, 2, 2, 4, 4, 3, 16>(a, s);
-        case EPI_QKV:     // 128 x 128, BK 16 (tiles may straddle the q|k|v sections: per-float4)
-            if (small_m) return launch<EPI_QKV, 1, 4, 1, 2, 2>(a, s);
+        case EPI_QKV:     // 128 x 96 (N = 864 / 6144) or 128 x 128 BK 16; per-float4 sections
+            if (small_m) return launch<EPI_QKV, 1, 4, 1, 2, 2, 32>(a, s);
+            if (a.N % 96 == 0) return launch<EPI_QKV, 2, 2, 4, 3, 4, 16>(a, s);
             return launch<EPI_QKV, 2, 2, 4, 4, 3, 16>(a, s);
         case EPI_RESID:   // O-proj / down
-            if (small_m) return launch<EPI_RESID, 1, 4, 1, 2, 2>(a, s);
+            if (small_m) return launch<EPI_RESID, 1, 4, 1, 2, 2, 32>(a, s);
             if (a.N % 96 == 0)
-                return a.K <= 512 ? launch<EPI_RESID, 2, 2, 2, 3, 2>(a, s)   // 64 x 96
-                                  : launch<EPI_RESID, 2, 2, 4, 3, 2>(a, s);  // 128 x 96
-            return launch<EPI_RESID, 2, 2, 4, 4, 3, 16>(a, s);               // 128 x 128
+                return a.K <= 512 ? launch<EPI_RESID, 2, 2, 2, 3, 3, 32>(a, s)   // 64 x 96
+                                  : launch<EPI_RESID, 2, 2, 4, 3, 2, 32>(a, s);  // 128 x 96
+            return launch<EPI_RESID, 2, 2, 4, 4, 3, 16>(a, s);                   // 128 x 128
         case EPI_STORE:   // lm_head, op-level linear
-            if (small_m) return launch<EPI_STORE, 1, 4, 1, 2, 2>(a, s);
+            if (small_m) return launch<EPI_STORE, 1, 4, 1, 2, 2, 32>(a, s);
             return launch<EPI_STORE, 2, 2, 4, 4, 3, 16>(a, s);
         default:
             return hipErrorInvalidValue;

@@ -244,24 +244,35 @@ __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
     dst[1] = rt;
 }
 
+// Quad swizzle of the unpadded LDS image row r (see gemm_lds_kernel).
+template <int BK>
+__device__ __forceinline__ int lds_swz(int r) {
+    return BK == 16 ? (r >> 1) & 3 : r & 7;
+}
+
 template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false,
-          int BK = 32, bool DIRECT = false>
+          int BK = 32, bool DIRECT = false, bool GLDS = false>
 __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
     constexpr int BM = WM * TM * 16;
     constexpr int BN = WN * TN * 16;
-    // LDS image rows: BK >= 32 -> padded stride BK + 8 (== 8 mod 16 floats: conflict-free
-    // ds_read_b128, and an 8-lane ds_write_b128 group writes one whole row).  BK = 16 -> no
-    // padding, float4 quad q of row r stored at quad q ^ ((r >> 1) & 3): the 8-lane write
-    // groups (two rows) and the 16-lane read groups (16 rows, one quad) both land on distinct
-    // banks (checked against the MI355X_MICROARCH.md lane groups), and the image is 1/3 smaller
-    constexpr bool SWZ = BK == 16;
-    constexpr int LDS_STRIDE = SWZ ? 16 : BK + 8;
+    // LDS image rows are unpadded (stride BK) with float4 quad q of row r stored at quad
+    // q ^ swz(r): BK 16 -> (r >> 1) & 3, BK 32 -> r & 7.  Both the ds_write_b128 groups (8 lanes:
+    // two rows at BK 16, one at BK 32) and the ds_read_b128 fragment reads (16-lane groups of
+    // MI355X_MICROARCH.md §LDS) are conflict-free (enumerated; the padded stride-24 BK16 image
+    // measured SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.32 from its writes), and unpadded
+    // rows let global_load_lds fill the image (GLDS) — 1 KB per wave-instruction
+    static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
+    constexpr int LDS_STRIDE = BK;
     constexpr int Q = BK / 4;           // float4 per staged row
-    static_assert(BK % 16 == 0 && (Q & (Q - 1)) == 0, "BK must be 16, 32 or 64");
     constexpr int A_F4 = BM * BK / 4;
     constexpr int B_F4 = BN * BK / 4;
     constexpr int A_IT = (A_F4 + 255) / 256;
     constexpr int B_IT = (B_F4 + 255) / 256;
+    // GLDS: k-tiles go global -> LDS by global_load_lds_dwordx4 (no staging VGPRs, no
+    // ds_write).  One wave-instruction fills 1 KB = RP rows of the image, lane i at byte 16 i;
+    // the swizzle moves to the source address (lane i loads logical quad (i % Q) ^ swz(r)).
+    static_assert(!GLDS || DIRECT, "GLDS copies A as stored: needs the folded norm (DIRECT)");
+    constexpr int RP = 256 / BK;  // image rows per 1 KB piece
 
     // one LDS array: [2][BM][stride] A image, then [2][BN][stride] B image; after the main
     // loop its head holds the per-row RMSNorm factors, then the staged output tile
@@ -327,7 +338,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
                     v *= wv;
                 }
                 const int r = f / Q, q = f % Q;
-                *reinterpret_cast<f32x4*>(&As[buf][r][(SWZ ? q ^ ((r >> 1) & 3) : q) * 4]) = v;
+                *reinterpret_cast<f32x4*>(&As[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = v;
             }
         }
 #pragma unroll
@@ -335,7 +346,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             const int f = tid + 256 * i;
             if (B_F4 % 256 == 0 || f < B_F4) {
                 const int r = f / Q, q = f % Q;
-                *reinterpret_cast<f32x4*>(&Bs[buf][r][(SWZ ? q ^ ((r >> 1) & 3) : q) * 4]) = rb[i];
+                *reinterpret_cast<f32x4*>(&Bs[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = rb[i];
             }
         }
     };
@@ -348,19 +359,20 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 
     const int frow = lane & 15, fk = 4 * (lane >> 4);
     const int arow0 = wm * TM * 16, brow0 = wn * TN * 16;
-    // fragment column in the image: rows 16i + frow share (frow >> 1) & 3 for the swizzle
-    const int fcol = SWZ ? 4 * ((lane >> 4) ^ ((frow >> 1) & 3)) : fk;
+    // fragment quad kg*4 + (lane>>4) of row 16i + frow: swz depends on frow only (16 | row base)
+    const int fswz = lds_swz<BK>(frow);
 
     auto compute = [&](int buf) {
 #pragma unroll
         for (int kg = 0; kg < BK / 16; ++kg) {
             f32x4 a[TM], bw[TN];
+            const int fcol = 4 * ((kg * 4 + (lane >> 4)) ^ fswz);
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(&As[buf][arow0 + i * 16 + frow][kg * 16 + fcol]);
+                a[i] = *reinterpret_cast<const f32x4*>(&As[buf][arow0 + i * 16 + frow][fcol]);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                bw[j] = *reinterpret_cast<const f32x4*>(&Bs[buf][brow0 + j * 16 + frow][kg * 16 + fcol]);
+                bw[j] = *reinterpret_cast<const f32x4*>(&Bs[buf][brow0 + j * 16 + frow][fcol]);
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -385,8 +397,38 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     f32x4 res[NRES];
 
     const int nk = p.K / BK;
-    gload(0);
-    sstore(0, 0);
+    // GLDS fill of one k-tile into image buf: 16-row pieces, BM/64 (A) and BN/64 (B) per wave;
+    // rows past M / N are clamped (their outputs are never stored)
+    auto glds_tile = [&](int buf, int k0) {
+        const int rl = lane / Q, pq = lane % Q;
+#pragma unroll
+        for (int it = 0; it < (BM / RP + 3) / 4; ++it) {
+            const int piece = wid + 4 * it, r = piece * RP + rl;  // pieces round-robin over waves
+            if ((BM / RP) % 4 == 0 || piece < BM / RP) {
+                const int gm = min(m0 + r, p.M - 1), q = pq ^ lds_swz<BK>(r);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(p.A + (int64_t)gm * p.lda + k0 + 4 * q),
+                    (__attribute__((address_space(3))) void*)&As[buf][piece * RP][0], 16, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < (BN / RP + 3) / 4; ++it) {
+            const int piece = wid + 4 * it, r = piece * RP + rl;
+            if ((BN / RP) % 4 == 0 || piece < BN / RP) {
+                const int gn = min(n0 + r, p.N - 1), q = pq ^ lds_swz<BK>(r);
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(p.W + (int64_t)gn * p.K + k0 + 4 * q),
+                    (__attribute__((address_space(3))) void*)&Bs[buf][piece * RP][0], 16, 0, 0);
+            }
+        }
+    };
+
+    if constexpr (GLDS) {
+        glds_tile(0, 0);
+    } else {
+        gload(0);
+        sstore(0, 0);
+    }
     __syncthreads();
     if constexpr (STAMP) {
         __builtin_amdgcn_sched_barrier(0);
@@ -395,10 +437,15 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     }
     for (int kt = 0; kt < nk - 1; ++kt) {
         const int cur = kt & 1;
-        gload((kt + 1) * BK);
-        compute(cur);
-        sstore(cur ^ 1, (kt + 1) * BK);
-        __syncthreads();
+        if constexpr (GLDS) {
+            glds_tile(cur ^ 1, (kt + 1) * BK);  // lands while this tile computes
+            compute(cur);
+        } else {
+            gload((kt + 1) * BK);
+            compute(cur);
+            sstore(cur ^ 1, (kt + 1) * BK);
+        }
+        __syncthreads();  // (GLDS: its fence waits vmcnt(0), retiring the DMA)
     }
     // last k-tile, peeled: its staging registers are dead, so the residual tile of EPI_RESID is
     // fetched here and its latency hides behind this tile's MFMAs

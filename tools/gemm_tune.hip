@@ -52,6 +52,13 @@ struct Variant {
                 hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
             }, true}
 
+#define GVAR(WM, WN, TM, TN, EPI, WPE, BK)                                                            \
+    Variant{"glds<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
+                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
+                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
+                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, true>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
+            }, true}
+
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
     for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;
@@ -224,17 +231,17 @@ int main(int argc, char** argv) {
     const bool c5 = argc > 3 && std::string(argv[3]) == "c5";
     if (!c5) {
     run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
-              {BVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), DVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
-               DVAR(2, 2, 4, 4, EPI_SWIGLU, 4, 16), DVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, iters);
+              {DVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
+               GVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, iters);
     run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
-              {BVAR(2, 2, 2, 3, EPI_QKV, 3, 16), DVAR(2, 2, 2, 3, EPI_QKV, 3, 16),
-               DVAR(2, 2, 4, 3, EPI_QKV, 3, 16), DVAR(2, 2, 4, 4, EPI_QKV, 3, 16)}, rounds, iters);
+              {DVAR(2, 2, 4, 4, EPI_QKV, 3, 16), GVAR(2, 2, 4, 4, EPI_QKV, 3, 16),
+               GVAR(2, 2, 4, 3, EPI_QKV, 3, 16), GVAR(2, 2, 4, 3, EPI_QKV, 4, 16)}, rounds, iters);
     run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
-              {BVAR(2, 2, 4, 3, EPI_RESID, 2, 32), DVAR(2, 2, 4, 3, EPI_RESID, 2, 32),
-               DVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
+              {DVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(2, 2, 4, 3, EPI_RESID, 2, 32),
+               GVAR(2, 2, 4, 3, EPI_RESID, 3, 32), GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
     run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
-              {BVAR(2, 2, 2, 3, EPI_RESID, 2, 32), DVAR(2, 2, 2, 3, EPI_RESID, 2, 32),
-               DVAR(2, 2, 2, 3, EPI_RESID, 3, 16), DVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
+              {DVAR(2, 2, 2, 3, EPI_RESID, 2, 32), GVAR(2, 2, 2, 3, EPI_RESID, 3, 32),
+               GVAR(2, 2, 2, 3, EPI_RESID, 3, 16), GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
     } else {
     // Llama-3-8B shapes (C5) at M = 16384 rows (tuning size)
     const int Mc = 16384;
