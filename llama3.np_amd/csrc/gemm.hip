@@ -53,16 +53,16 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         case EPI_SWIGLU:  // 128 x 128, BK 16
             if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2, 32>(a, s);
             return launch<EPI_SWIGLU, 2, 2, 4, 4, 3, 16>(a, s);
-        case EPI_QKV:     // 128 x 96 (N = 864 / 6144) or 128 x 128 BK 16; per-float4 sections
+        case EPI_QKV:     // 128 x 96 at short K (stories15M), else 128 x 128; BK 16
             if (small_m) return launch<EPI_QKV, 1, 4, 1, 2, 2, 32>(a, s);
-            if (a.N % 96 == 0) return launch<EPI_QKV, 2, 2, 4, 3, 4, 16>(a, s);
+            if (a.N % 96 == 0 && a.K <= 1024) return launch<EPI_QKV, 2, 2, 4, 3, 4, 16>(a, s);
             return launch<EPI_QKV, 2, 2, 4, 4, 3, 16>(a, s);
         case EPI_RESID:   // O-proj / down
             if (small_m) return launch<EPI_RESID, 1, 4, 1, 2, 2, 32>(a, s);
             if (a.N % 96 == 0)
                 return a.K <= 512 ? launch<EPI_RESID, 2, 2, 2, 3, 3, 32>(a, s)   // 64 x 96
                                   : launch<EPI_RESID, 2, 2, 4, 3, 2, 32>(a, s);  // 128 x 96
-            return launch<EPI_RESID, 2, 2, 4, 4, 3, 16>(a, s);                   // 128 x 128
+            return launch<EPI_RESID, 2, 2, 4, 4, 2, 32>(a, s);                   // 128 x 128
         case EPI_STORE:   // lm_head, op-level linear
             if (small_m) return launch<EPI_STORE, 1, 4, 1, 2, 2, 32>(a, s);
             return launch<EPI_STORE, 2, 2, 4, 4, 3, 16>(a, s);

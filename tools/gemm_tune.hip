@@ -246,17 +246,15 @@ int main(int argc, char** argv) {
     // Llama-3-8B shapes (C5) at M = 16384 rows (tuning size)
     const int Mc = 16384;
     run_shape("C5 gate|up", EPI_SWIGLU, Mc, 4096, 28672, true,
-              {BVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32), BVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 16),
-               BVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16)}, rounds, 3);
+              {DVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
+               GVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, 3);
     run_shape("C5 QKV-shape (store)", EPI_STORE, Mc, 4096, 6144, true,
-              {BVAR(2, 2, 4, 3, EPI_STORE, 2, 32), BVAR(2, 2, 2, 3, EPI_STORE, 3, 16),
-               BVAR(2, 2, 4, 4, EPI_STORE, 2, 16), BVAR(2, 2, 4, 3, EPI_STORE, 3, 16)}, rounds, 3);
+              {GVAR(2, 2, 4, 4, EPI_STORE, 3, 16), GVAR(2, 2, 4, 3, EPI_STORE, 4, 16),
+               GVAR(2, 2, 4, 4, EPI_STORE, 2, 32)}, rounds, 3);
     run_shape("C5 O-proj", EPI_RESID, Mc, 4096, 4096, false,
-              {BVAR(2, 2, 2, 4, EPI_RESID, 2, 32), BVAR(2, 2, 4, 4, EPI_RESID, 2, 16),
-               BVAR(2, 2, 2, 4, EPI_RESID, 3, 16), BVAR(2, 2, 4, 4, EPI_RESID, 2, 32)}, rounds, 3);
+              {GVAR(2, 2, 4, 4, EPI_RESID, 3, 16), GVAR(2, 2, 4, 4, EPI_RESID, 2, 32)}, rounds, 3);
     run_shape("C5 down", EPI_RESID, Mc, 14336, 4096, false,
-              {BVAR(2, 2, 2, 4, EPI_RESID, 2, 32), BVAR(2, 2, 4, 4, EPI_RESID, 2, 16),
-               BVAR(2, 2, 2, 4, EPI_RESID, 3, 16)}, rounds, 3);
+              {GVAR(2, 2, 4, 4, EPI_RESID, 3, 16), GVAR(2, 2, 4, 4, EPI_RESID, 2, 32)}, rounds, 3);
     }
     return 0;
 }
