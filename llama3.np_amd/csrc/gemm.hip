@@ -11,7 +11,7 @@ template <int EPI, int WM, int WN, int TM, int TN, int WPE, int BK>
 static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, true>),
+    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>),
                        dim3((unsigned)tiles), dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -34,7 +34,6 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.K % 32 != 0 || a.K <= 0) return hipErrorInvalidValue;  // whole 32-deep k-tiles
     if (epi == EPI_SWIGLU && a.N % 32 != 0) return hipErrorInvalidValue;
     if (a.N % 4 != 0 || a.ldc % 4 != 0 || a.lda % 4 != 0) return hipErrorInvalidValue;  // 16-B rows
-    if (a.norm_w) return hipErrorInvalidValue;  // norm weights are folded into W (l3_finalize)
     // M <= 8 (decode, short prompts): weight-streaming GEMV with the same epilogues
     const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
     if (a.M <= 8 && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS

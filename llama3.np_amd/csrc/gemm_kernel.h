@@ -10,30 +10,30 @@
 //
 // Matrix core: v_mfma_f32_16x16x4_f32 (exact fp32 in / fp32 accumulate, 64 FLOP/clk/SIMD,
 // 157.3 TF/s chip peak).  Fragment maps (cdna_hip_programming.md section 3):
-//   A: lane l supplies A[i = l&15][k = l>>4];  B: lane l supplies B[k = l>>4][j = l&15];
+//   A operand: lane l supplies A[i = l&15][k = l>>4];  B operand: lane l supplies B[k = l>>4][j = l&15];
 //   C/D: lane l holds C[row = 4*(l>>4) + r][col = l&15], r = 0..3.
-// K-permutation trick: a sum over k may visit k in any order as long as A and B agree, so at
-// sub-step s lane l feeds k = G*(l>>4) + s for a group of 4G k values (G = 4 or 8).  One
-// 16-byte read of a K-contiguous row then yields the operands of four consecutive MFMAs, for
-// A and for W alike (both are stored K-contiguous: W is the reference's [out, in]).
+// K-permutation trick: a sum over k may visit k in any order as long as both operands agree,
+// so at sub-step s lane l feeds k = 4*(l>>4) + s of a 16-deep group: one 16-byte LDS read of a
+// K-contiguous row yields the operands of four consecutive MFMAs, for the activations and for
+// W alike (both K-contiguous: W is the reference's [out, in]).
 //
-// Main loop: K staged 32 deep through a double-buffered LDS image (row stride 40 floats == 8
-// mod 16: conflict-free ds_read_b128), register prefetch one tile ahead, one barrier per tile;
-// 80 KB of LDS so two blocks share a CU (measured: 1 block/CU -23%).  Rejected after
-// measurement (tools/gemm_tune): an LDS-free variant streaming fragment-shaped
-// loads straight to VGPRs (-35%) and a persistent flattened (tile, k) pipeline (-7%).
+// Operands are swapped (W fragment as the A operand, activation fragment as B), so every
+// accumulator is C^T: lane l holds C[row = 16i + (l&15)][col = 16j + 4(l>>4) + r] — four
+// consecutive columns of one row, stored with one 16-byte write straight from registers (no
+// LDS staging, no block barrier after the main loop).
 //
-// Epilogue: values are finished in registers (RMSNorm row factor, SwiGLU), staged
-// through the now idle LDS as a row-major tile, and written back as full rows with 16-byte
-// stores (RoPE is applied there, on float4s holding whole pairs); the residual tile of
-// EPI_RESID is fetched into registers during the last k-tile so its latency hides behind the
-// MFMAs.  (Row-per-lane 4-byte stores cost 18k-50k cycles
-// per block in-kernel-stamped diagnostics — up to 60% of the main loop.)
+// Main loop: K staged BK (16 or 32) deep through a double-buffered, unpadded, XOR-swizzled LDS
+// image, one tile in flight ahead, one barrier per k-tile.  The next tile is filled either by
+// global_load_lds (GLDS, the product path: no staging VGPRs, 128 x 128 fits 4 blocks/CU) or by
+// register staging + ds_write_b128.  Rejected after measurement (tools/gemm_tune):
+// fragment-shaped global loads straight to VGPRs (-35 %), a persistent flattened (tile, k)
+// pipeline (-7 %), an LDS-staged row-major epilogue (-4 %).
 //
-// RMSNorm fusion: rmsnorm(x) @ W^T = diag(1/rms(x)) * (x * w_norm) @ W^T.  The norm weight
-// multiplies the A values in registers, the per-row sum of squares is accumulated from the same
-// registers, and 1/rms scales the rows in the epilogue — the normalised activations are never
-// written to HBM and W stays as stored.
+// RMSNorm fusion: rmsnorm(x) @ W^T = diag(1/rms(x)) * x @ (W * w_norm)^T.  The norm weight is
+// folded into W's columns once (l3_finalize, fold_cols_kernel); each lane accumulates the sum
+// of squares of the A values its own fragments carry (a quarter of K of its row), two
+// shuffles complete the row, and 1/rms scales the accumulators — the normalised activations
+// are never materialised and A is copied to LDS as stored.
 #pragma once
 #include "kernels.h"
 
@@ -54,121 +54,22 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
     return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
 }
 
-// Output tile geometry of the staged epilogue.
-template <int BM, int BN, int EPI>
-struct OutTile {
-    static constexpr int COLS = EPI == EPI_SWIGLU ? BN / 2 : BN;  // output columns of the tile
-    static constexpr int STRIDE = COLS + 4;  // == 4 mod 8: the two row groups of a wave's
-                                             // ds_write_b32 land on disjoint banks
-    static constexpr int F4 = BM * COLS / 4;
-    static constexpr int IT = (F4 + 255) / 256;
-    // EPI_RESID: prefetch the residual tile into registers during the last k-tile when it is
-    // at most 12 float4 per thread (64x96, 128x96); larger tiles (128x128, long-K shapes) load
-    // it in the store phase instead of spilling
-    static constexpr bool RES_PREFETCH = IT <= 12;
-};
-
-// Phase 1+2: finish the wave's TM x TN accumulator tiles in registers and stage them,
-// row-major, into stage[BM][STRIDE].  rloc/cloc: the wave tile's first row/col in the block
-// tile; scale(i, r): RMSNorm factor of local row rloc + 16i + 4(lane>>4) + r.
-template <int BM, int BN, int TM, int TN, int EPI, typename Scale>
-__device__ __forceinline__ void stage_tile(const GemmArgs& p, f32x4 (&acc)[TM][TN], float* stage,
-                                           int m0, int n0, int rloc, int cloc, int lane,
-                                           Scale scale) {
-    using O = OutTile<BM, BN, EPI>;
-    const int frow = lane & 15, fq4 = 4 * (lane >> 4);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int lrow = rloc + i * 16 + fq4 + r;
-            const float sc = scale(i, r);
-            float* srow = stage + lrow * O::STRIDE;
-            if constexpr (EPI == EPI_SWIGLU) {
-#pragma unroll
-                for (int j = 0; j < TN; j += 2)
-                    srow[(cloc + j * 16) / 2 + frow] = silu_f(acc[i][j][r] * sc) * (acc[i][j + 1][r] * sc);
-            } else {
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    srow[cloc + j * 16 + frow] = EPI == EPI_RESID ? acc[i][j][r] : acc[i][j][r] * sc;
-            }
-        }
-    }
+// Quad swizzle of row r of the unpadded LDS image: float4 quad q is stored at q ^ lds_swz(r).
+// BK 16 -> (r >> 1) & 3, BK 32 -> r & 7: the ds_write_b128 groups (8 lanes: two rows at BK 16,
+// one at BK 32) and the ds_read_b128 fragment reads (the four 16-lane groups of
+// MI355X_MICROARCH.md section LDS) are conflict-free — enumerated, and the padded stride-24
+// image it replaced measured SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.32 from its writes.
+template <int BK>
+__device__ __forceinline__ int lds_swz(int r) {
+    return BK == 16 ? (r >> 1) & 3 : r & 7;
 }
 
-// Residual prefetch for EPI_RESID: the same row-major float4 map phase 3 uses.
-template <int BM, int BN, int EPI, int NR>
-__device__ __forceinline__ void load_residual(const GemmArgs& p, f32x4 (&res)[NR],
-                                              int m0, int n0, int tid) {
-    using O = OutTile<BM, BN, EPI>;
-#pragma unroll
-    for (int i = 0; i < O::IT; ++i) {
-        const int f = tid + 256 * i;
-        const int lrow = f / (O::COLS / 4), col = n0 + (f % (O::COLS / 4)) * 4;
-        const int row = m0 + lrow;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if ((O::F4 % 256 == 0 || f < O::F4) && row < p.M && col < p.N)
-            v = *reinterpret_cast<const f32x4*>(p.C + (int64_t)row * p.ldc + col);
-        res[i] = v;
-    }
-}
-
-// Phase 3: full-row 16-byte stores of the staged tile (after a barrier).  Column counts are
-// multiples of 4 (checked by launch_gemm), so a float4 never crosses the matrix edge or a
-// q|k|v section / head boundary.
-template <int BM, int BN, int EPI, int NR>
-__device__ __forceinline__ void store_tile(const GemmArgs& p, const float* stage,
-                                           const f32x4 (&res)[NR], int m0,
-                                           int n0, int tid) {
-    using O = OutTile<BM, BN, EPI>;
-    const int ncols = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
-    const int c0 = EPI == EPI_SWIGLU ? n0 / 2 : n0;
-#pragma unroll
-    for (int i = 0; i < O::IT; ++i) {
-        const int f = tid + 256 * i;
-        if (!(O::F4 % 256 == 0 || f < O::F4)) continue;
-        const int lrow = f / (O::COLS / 4), lc = (f % (O::COLS / 4)) * 4;
-        const int row = m0 + lrow, col = c0 + lc;
-        if (row >= p.M || col >= ncols) continue;
-        f32x4 v = *reinterpret_cast<const f32x4*>(stage + lrow * O::STRIDE + lc);
-        if constexpr (EPI == EPI_QKV) {
-            // RoPE here, where a float4 holds two whole (even, odd) pairs: one 8-byte cos and
-            // one 8-byte sin load per float4 (llama3.py:41-76), then q scaling / cache append
-            const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
-            const int bidx = row / p.L, pos = start_of(p) + row - bidx * p.L;
-            const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
-            const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
-            const int head = cc / p.HD, d = cc - head * p.HD;
-            if (is_q || is_k) {
-                const int t = pos * (p.HD >> 1) + (d >> 1);
-                const float2 c = *reinterpret_cast<const float2*>(p.rope_cos + t);
-                const float2 sn = *reinterpret_cast<const float2*>(p.rope_sin + t);
-                v = f32x4{v.x * c.x - v.y * sn.x, v.x * sn.x + v.y * c.x,
-                          v.z * c.y - v.w * sn.y, v.z * sn.y + v.w * c.y};
-            }
-            if (is_q) {
-                *reinterpret_cast<f32x4*>(p.q_out + (int64_t)row * qdim + col) = v * p.q_scale;
-            } else {
-                float* cache = is_k ? p.cache_k : p.cache_v;
-                *reinterpret_cast<f32x4*>(cache + (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d) = v;
-            }
-        } else {
-            if constexpr (EPI == EPI_RESID) {
-                if constexpr (O::RES_PREFETCH) v += res[i];
-                else v += *reinterpret_cast<const f32x4*>(p.C + (int64_t)row * p.ldc + col);
-            }
-            *reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + col) = v;
-        }
-    }
-}
-
-// Register-direct epilogue (DIRECT kernels).  The MFMA operands are swapped (W fragment as
+// Register-direct epilogue.  The MFMA operands are swapped (W fragment as
 // the A operand, activation fragment as B), so the accumulator of tile (i, j) is C^T: lane l
 // holds C[row = 16i + (l&15)][col = 16j + 4(l>>4) + r], r = 0..3 — four consecutive columns
 // of one row, i.e. one 16-byte store, with no LDS staging and no block barrier.  rs[i] is the
 // lane's RMSNorm factor for its row of tile i (1 without norm); res the prefetched residual.
-template <int TM, int TN, int EPI, int NR>
+template <int TM, int TN, int EPI, bool RES_PREFETCH, int NR>
 __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (&acc)[TM][TN],
                                                 const float (&rs)[TM], const f32x4 (&res)[NR],
                                                 int mrow0, int ncol0, int lane) {
@@ -220,7 +121,7 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
                 } else {
                     float* dst = p.C + (int64_t)row * p.ldc + col;
                     if constexpr (EPI == EPI_RESID) {
-                        if constexpr (NR == TM * TN) v += res[i * TN + j];
+                        if constexpr (RES_PREFETCH) v += res[i * TN + j];
                         else v += *reinterpret_cast<const f32x4*>(dst);
                     } else {
                         v *= sc;
@@ -232,9 +133,6 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// LDS-staged main loop
-
 // In-kernel clock stamps for diagnostic builds (never in the product path): shader-clock
 // counter and the 100 MHz real-time counter, read together.
 __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
@@ -244,166 +142,47 @@ __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
     dst[1] = rt;
 }
 
-// Quad swizzle of the unpadded LDS image row r (see gemm_lds_kernel).
-template <int BK>
-__device__ __forceinline__ int lds_swz(int r) {
-    return BK == 16 ? (r >> 1) & 3 : r & 7;
-}
+#define L3_STAMP(slot)                             \
+    if constexpr (STAMP) {                         \
+        __builtin_amdgcn_sched_barrier(0);         \
+        stamp_pair(stamps + 2 * (slot));           \
+        __builtin_amdgcn_sched_barrier(0);         \
+    }
 
+// ---------------------------------------------------------------------------------------
+// Tiled kernel: 256 threads = 4 waves as WM x WN, wave tile (TM x 16) x (TN x 16).
 template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false,
-          int BK = 32, bool DIRECT = false, bool GLDS = false>
+          int BK = 32, bool GLDS = true>
 __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
     constexpr int BM = WM * TM * 16;
     constexpr int BN = WN * TN * 16;
-    // LDS image rows are unpadded (stride BK) with float4 quad q of row r stored at quad
-    // q ^ swz(r): BK 16 -> (r >> 1) & 3, BK 32 -> r & 7.  Both the ds_write_b128 groups (8 lanes:
-    // two rows at BK 16, one at BK 32) and the ds_read_b128 fragment reads (16-lane groups of
-    // MI355X_MICROARCH.md §LDS) are conflict-free (enumerated; the padded stride-24 BK16 image
-    // measured SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.32 from its writes), and unpadded
-    // rows let global_load_lds fill the image (GLDS) — 1 KB per wave-instruction
     static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
-    constexpr int LDS_STRIDE = BK;
-    constexpr int Q = BK / 4;           // float4 per staged row
-    constexpr int A_F4 = BM * BK / 4;
-    constexpr int B_F4 = BN * BK / 4;
-    constexpr int A_IT = (A_F4 + 255) / 256;
-    constexpr int B_IT = (B_F4 + 255) / 256;
-    // GLDS: k-tiles go global -> LDS by global_load_lds_dwordx4 (no staging VGPRs, no
-    // ds_write).  One wave-instruction fills 1 KB = RP rows of the image, lane i at byte 16 i;
-    // the swizzle moves to the source address (lane i loads logical quad (i % Q) ^ swz(r)).
-    static_assert(!GLDS || DIRECT, "GLDS copies A as stored: needs the folded norm (DIRECT)");
-    constexpr int RP = 256 / BK;  // image rows per 1 KB piece
+    constexpr int Q = BK / 4;        // float4 per image row
+    constexpr int RP = 256 / BK;     // image rows per 1 KB global_load_lds piece
+    constexpr int A_F4 = BM * Q, B_F4 = BN * Q;
+    constexpr int A_IT = (A_F4 + 255) / 256, B_IT = (B_F4 + 255) / 256;
 
-    // one LDS array: [2][BM][stride] A image, then [2][BN][stride] B image; after the main
-    // loop its head holds the per-row RMSNorm factors, then the staged output tile
-    constexpr int MAIN_F = 2 * (BM + BN) * LDS_STRIDE;
-    constexpr int EPI_F = DIRECT ? 0 : ((BM + 3) & ~3) + BM * OutTile<BM, BN, EPI>::STRIDE;
-    __shared__ __attribute__((aligned(16))) float smem[MAIN_F > EPI_F ? MAIN_F : EPI_F];
-    float (*As)[BM][LDS_STRIDE] = reinterpret_cast<float (*)[BM][LDS_STRIDE]>(smem);
-    float (*Bs)[BN][LDS_STRIDE] = reinterpret_cast<float (*)[BN][LDS_STRIDE]>(smem + 2 * BM * LDS_STRIDE);
-    float* row_scale = smem;
+    // one LDS array: [2][BM][BK] A image, then [2][BN][BK] W image
+    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * BK];
+    float (*As)[BM][BK] = reinterpret_cast<float (*)[BM][BK]>(smem);
+    float (*Bs)[BN][BK] = reinterpret_cast<float (*)[BN][BK]>(smem + 2 * BM * BK);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     const int ntn = (p.N + BN - 1) / BN;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
-    unsigned long long stamps[12];
-    if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps);
-        __builtin_amdgcn_sched_barrier(0);
-    }
+    unsigned long long stamps[8];
+    L3_STAMP(0);
 
-    f32x4 ra[A_IT], rb[B_IT];
-    // RMSNorm sums of squares: per staged A row (LDS epilogue) or, DIRECT, per lane from its
-    // own A fragments (row 16i + (lane&15) of the wave tile, a quarter of K per lane)
-    constexpr int NSS = DIRECT ? TM : A_IT;
-    float ss[NSS];
-#pragma unroll
-    for (int i = 0; i < NSS; ++i) ss[i] = 0.f;
-
-    auto gload = [&](int k0) {
-#pragma unroll
-        for (int i = 0; i < A_IT; ++i) {
-            const int f = tid + 256 * i;
-            const int row = f / Q, c = (f % Q) * 4;
-            const int gm = m0 + row;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((A_F4 % 256 == 0 || f < A_F4) && gm < p.M)
-                v = *reinterpret_cast<const f32x4*>(p.A + (int64_t)gm * p.lda + k0 + c);
-            ra[i] = v;
-        }
-#pragma unroll
-        for (int i = 0; i < B_IT; ++i) {
-            const int f = tid + 256 * i;
-            const int row = f / Q, c = (f % Q) * 4;
-            const int gn = n0 + row;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((B_F4 % 256 == 0 || f < B_F4) && gn < p.N)
-                v = *reinterpret_cast<const f32x4*>(p.W + (int64_t)gn * p.K + k0 + c);
-            rb[i] = v;
-        }
-    };
-    auto sstore = [&](int buf, int k0) {
-        f32x4 wv = {1.f, 1.f, 1.f, 1.f};
-        if (!DIRECT && p.norm) wv = *reinterpret_cast<const f32x4*>(p.norm_w + k0 + (tid % Q) * 4);
-#pragma unroll
-        for (int i = 0; i < A_IT; ++i) {
-            const int f = tid + 256 * i;  // f % Q == tid % Q: one norm-weight quad per thread
-            if (A_F4 % 256 == 0 || f < A_F4) {
-                f32x4 v = ra[i];
-                if (!DIRECT && p.norm) {
-                    ss[i] += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-                    v *= wv;
-                }
-                const int r = f / Q, q = f % Q;
-                *reinterpret_cast<f32x4*>(&As[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = v;
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < B_IT; ++i) {
-            const int f = tid + 256 * i;
-            if (B_F4 % 256 == 0 || f < B_F4) {
-                const int r = f / Q, q = f % Q;
-                *reinterpret_cast<f32x4*>(&Bs[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = rb[i];
-            }
-        }
-    };
-
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    const int frow = lane & 15, fk = 4 * (lane >> 4);
-    const int arow0 = wm * TM * 16, brow0 = wn * TN * 16;
-    // fragment quad kg*4 + (lane>>4) of row 16i + frow: swz depends on frow only (16 | row base)
-    const int fswz = lds_swz<BK>(frow);
-
-    auto compute = [&](int buf) {
-#pragma unroll
-        for (int kg = 0; kg < BK / 16; ++kg) {
-            f32x4 a[TM], bw[TN];
-            const int fcol = 4 * ((kg * 4 + (lane >> 4)) ^ fswz);
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-                a[i] = *reinterpret_cast<const f32x4*>(&As[buf][arow0 + i * 16 + frow][fcol]);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                bw[j] = *reinterpret_cast<const f32x4*>(&Bs[buf][brow0 + j * 16 + frow][fcol]);
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = DIRECT ? mfma4(bw[j][s], a[i][s], acc[i][j])
-                                           : mfma4(a[i][s], bw[j][s], acc[i][j]);
-            if constexpr (DIRECT) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-                    ss[i] += a[i].x * a[i].x + a[i].y * a[i].y + a[i].z * a[i].z + a[i].w * a[i].w;
-            }
-        }
-    };
-
-    // residual prefetch (EPI_RESID): LDS epilogue -> its row-major float4 map; DIRECT -> the
-    // lane's own (row, 4 columns) of every accumulator tile, when at most 12 float4
-    constexpr bool DIRECT_RES = DIRECT && EPI == EPI_RESID && TM * TN <= 12;
-    constexpr int NRES = DIRECT ? (DIRECT_RES ? TM * TN : 1)
-                                : (OutTile<BM, BN, EPI>::RES_PREFETCH ? OutTile<BM, BN, EPI>::IT : 1);
-    f32x4 res[NRES];
-
-    const int nk = p.K / BK;
-    // GLDS fill of one k-tile into image buf: 16-row pieces, BM/64 (A) and BN/64 (B) per wave;
-    // rows past M / N are clamped (their outputs are never stored)
+    // ---- k-tile fill, GLDS: one wave-instruction writes 1 KB = RP image rows (lane i at byte
+    // 16 i); the swizzle moves to the source address.  Pieces go round-robin over the waves;
+    // rows past M / N are clamped (their outputs are never stored).
     auto glds_tile = [&](int buf, int k0) {
         const int rl = lane / Q, pq = lane % Q;
 #pragma unroll
         for (int it = 0; it < (BM / RP + 3) / 4; ++it) {
-            const int piece = wid + 4 * it, r = piece * RP + rl;  // pieces round-robin over waves
+            const int piece = wid + 4 * it, r = piece * RP + rl;
             if ((BM / RP) % 4 == 0 || piece < BM / RP) {
                 const int gm = min(m0 + r, p.M - 1), q = pq ^ lds_swz<BK>(r);
                 __builtin_amdgcn_global_load_lds(
@@ -422,19 +201,90 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             }
         }
     };
+    // ---- k-tile fill, register staging: float4 f of the tile -> row f / Q, quad f % Q
+    f32x4 ra[GLDS ? 1 : A_IT], rb[GLDS ? 1 : B_IT];
+    auto gload = [&](int k0) {
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+            const int f = tid + 256 * i, row = f / Q, c = (f % Q) * 4, gm = m0 + row;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((A_F4 % 256 == 0 || f < A_F4) && gm < p.M)
+                v = *reinterpret_cast<const f32x4*>(p.A + (int64_t)gm * p.lda + k0 + c);
+            ra[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i) {
+            const int f = tid + 256 * i, row = f / Q, c = (f % Q) * 4, gn = n0 + row;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((B_F4 % 256 == 0 || f < B_F4) && gn < p.N)
+                v = *reinterpret_cast<const f32x4*>(p.W + (int64_t)gn * p.K + k0 + c);
+            rb[i] = v;
+        }
+    };
+    auto sstore = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+            const int f = tid + 256 * i, r = f / Q, q = f % Q;
+            if (A_F4 % 256 == 0 || f < A_F4)
+                *reinterpret_cast<f32x4*>(&As[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = ra[i];
+        }
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i) {
+            const int f = tid + 256 * i, r = f / Q, q = f % Q;
+            if (B_F4 % 256 == 0 || f < B_F4)
+                *reinterpret_cast<f32x4*>(&Bs[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = rb[i];
+        }
+    };
 
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss[TM];  // RMSNorm: sum of squares of this lane's quarter of row 16i + (lane & 15)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) ss[i] = 0.f;
+
+    const int frow = lane & 15, fk = 4 * (lane >> 4);
+    const int arow0 = wm * TM * 16, brow0 = wn * TN * 16;
+    const int fswz = lds_swz<BK>(frow);  // rows 16i + frow share it (16 | row base)
+
+    auto compute = [&](int buf) {
+#pragma unroll
+        for (int kg = 0; kg < BK / 16; ++kg) {
+            f32x4 a[TM], bw[TN];
+            const int fcol = 4 * ((kg * 4 + (lane >> 4)) ^ fswz);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = *reinterpret_cast<const f32x4*>(&As[buf][arow0 + i * 16 + frow][fcol]);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bw[j] = *reinterpret_cast<const f32x4*>(&Bs[buf][brow0 + j * 16 + frow][fcol]);
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma4(bw[j][s], a[i][s], acc[i][j]);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                ss[i] += a[i].x * a[i].x + a[i].y * a[i].y + a[i].z * a[i].z + a[i].w * a[i].w;
+        }
+    };
+
+    // EPI_RESID: the lane's residual float4s, prefetched during the last k-tile when at most 12
+    constexpr bool RES_PREFETCH = EPI == EPI_RESID && TM * TN <= 12;
+    f32x4 res[RES_PREFETCH ? TM * TN : 1];
+
+    const int nk = p.K / BK;
     if constexpr (GLDS) {
         glds_tile(0, 0);
     } else {
         gload(0);
-        sstore(0, 0);
+        sstore(0);
     }
     __syncthreads();
-    if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps + 2);
-        __builtin_amdgcn_sched_barrier(0);
-    }
+    L3_STAMP(1);
     for (int kt = 0; kt < nk - 1; ++kt) {
         const int cur = kt & 1;
         if constexpr (GLDS) {
@@ -443,13 +293,13 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         } else {
             gload((kt + 1) * BK);
             compute(cur);
-            sstore(cur ^ 1, (kt + 1) * BK);
+            sstore(cur ^ 1);
         }
         __syncthreads();  // (GLDS: its fence waits vmcnt(0), retiring the DMA)
     }
-    // last k-tile, peeled: its staging registers are dead, so the residual tile of EPI_RESID is
-    // fetched here and its latency hides behind this tile's MFMAs
-    if constexpr (DIRECT_RES) {
+    // last k-tile, peeled: the residual loads are issued first so their latency hides behind
+    // this tile's MFMAs
+    if constexpr (RES_PREFETCH) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -459,98 +309,35 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
                                       ? *reinterpret_cast<const f32x4*>(p.C + (int64_t)row * p.ldc + col)
                                       : f32x4{0.f, 0.f, 0.f, 0.f};
             }
-    } else if constexpr (!DIRECT && EPI == EPI_RESID && OutTile<BM, BN, EPI>::RES_PREFETCH) {
-        load_residual<BM, BN, EPI>(p, res, m0, n0, tid);
     }
     compute((nk - 1) & 1);
 
-    if constexpr (DIRECT) {
-        // no barrier: each wave finishes its own tile from registers
-        float rs[TM];
-        const float inv_k = 1.0f / (float)p.K;
+    // no barrier: each wave finishes its own tile from registers
+    float rs[TM];
+    const float inv_k = 1.0f / (float)p.K;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            float v = ss[i];
-            v += __shfl_xor(v, 16);  // the four k-quarters of the row
-            v += __shfl_xor(v, 32);
-            rs[i] = p.norm ? 1.0f / sqrtf(v * inv_k + p.eps) : 1.0f;
-        }
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            stamp_pair(stamps + 4);
-            stamp_pair(stamps + 6);
-            stamp_pair(stamps + 8);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        direct_epilogue<TM, TN, EPI>(p, acc, rs, res, m0 + arow0, n0 + brow0, lane);
-        if constexpr (STAMP) {
-            __builtin_amdgcn_sched_barrier(0);
-            stamp_pair(stamps + 10);
-            if (tid == 0) {
-                unsigned long long* d = p.stamps + (size_t)blockIdx.x * 14;
-                for (int i = 0; i < 12; ++i) d[i] = stamps[i];
-                d[12] = 0;
-                d[13] = t;
-            }
-        }
-        return;
+    for (int i = 0; i < TM; ++i) {
+        float v = ss[i];
+        v += __shfl_xor(v, 16);  // the four k-quarters of the row
+        v += __shfl_xor(v, 32);
+        rs[i] = p.norm ? 1.0f / sqrtf(v * inv_k + p.eps) : 1.0f;
     }
-    __syncthreads();
-
-    if (p.norm) {
-        const float inv_k = 1.0f / (float)p.K;
-#pragma unroll
-        for (int i = 0; i < A_IT; ++i) {
-            float v = ss[i];
-#pragma unroll
-            for (int o = 1; o < Q; o <<= 1) v += __shfl_xor(v, o);  // the Q lanes of one row
-            const int f = tid + 256 * i;
-            if ((tid % Q) == 0 && (A_F4 % 256 == 0 || f < A_F4))
-                row_scale[f / Q] = 1.0f / sqrtf(v * inv_k + p.eps);
-        }
-        __syncthreads();
-    }
-    const bool nrm = p.norm;
+    L3_STAMP(2);
+    direct_epilogue<TM, TN, EPI, RES_PREFETCH>(p, acc, rs, res, m0 + arow0, n0 + brow0, lane);
+    L3_STAMP(3);
     if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps + 4);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // staged epilogue: the tile goes after the row factors in the (idle) LDS array
-    float* stage = smem + ((BM + 3) & ~3);
-    float sc_reg[TM][4];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sc_reg[i][r] = nrm ? row_scale[arow0 + i * 16 + fk + r] : 1.0f;
-    stage_tile<BM, BN, TM, TN, EPI>(p, acc, stage, m0, n0, arow0, brow0, lane,
-                                    [&](int i, int r) { return sc_reg[i][r]; });
-    if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps + 6);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();
-    if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps + 8);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    store_tile<BM, BN, EPI>(p, stage, res, m0, n0, tid);
-    if constexpr (STAMP) {
-        __builtin_amdgcn_sched_barrier(0);
-        stamp_pair(stamps + 10);
         if (tid == 0) {
-            unsigned long long* d = p.stamps + (size_t)blockIdx.x * 14;
-            for (int i = 0; i < 12; ++i) d[i] = stamps[i];
+            unsigned long long* d = p.stamps + (size_t)blockIdx.x * 10;
+            for (int i = 0; i < 8; ++i) d[i] = stamps[i];
             unsigned xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            d[12] = xcc;
-            d[13] = t;
+            d[8] = xcc;
+            d[9] = t;
         }
     }
 }
 
+#undef L3_STAMP
 
 // ---------------------------------------------------------------------------------------
 // Skinny GEMM for M <= 8 rows (greedy decode, short prompts): the op is weight-streaming

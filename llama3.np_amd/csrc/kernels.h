@@ -20,8 +20,6 @@ struct GemmArgs {
     int M, N, K;
     bool norm;                     // RMSNorm on A: rows scaled by 1/sqrt(mean(A^2)+eps); the norm
                                    // weight is folded into W's columns (launch_fold_cols)
-    const float* norm_w;           // must be null for launch_gemm (folded); the LDS-epilogue
-                                   // kernels in tools/gemm_tune still multiply A by it
     float eps;
     // EPI_QKV
     float* q_out;                  // [M, H*HD], pre-scaled by q_scale
@@ -30,7 +28,7 @@ struct GemmArgs {
     int L, start_pos, H, KVH, HD, Smax;
     const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
-    unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 14 per block
+    unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 10 per block
 };
 
 struct AttnArgs {

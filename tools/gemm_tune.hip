@@ -27,37 +27,17 @@ using namespace l3;
 struct Variant {
     std::string name;
     std::function<void(const GemmArgs&, hipStream_t)> run;
-    bool direct = false;  // register-direct epilogue: takes W with the norm weight folded in
 };
 
-
-#define VAR(KERNEL, WM, WN, TM, TN, EPI, WPE)                                                       \
-    Variant{#KERNEL "<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ">", [](const GemmArgs& a, hipStream_t s) { \
+// RVAR: k-tiles by register staging + ds_write_b128; GVAR: by global_load_lds (product path)
+#define TVAR(TAG, GL, WM, WN, TM, TN, EPI, WPE, BK)                                                   \
+    Variant{TAG "<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
                 constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
                 const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
-                hipLaunchKernelGGL((KERNEL<WM, WN, TM, TN, EPI, WPE, false>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
+                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, GL>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
             }}
-
-#define BVAR(WM, WN, TM, TN, EPI, WPE, BK)                                                            \
-    Variant{"lds<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
-                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
-                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
-                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
-            }}
-
-#define DVAR(WM, WN, TM, TN, EPI, WPE, BK)                                                            \
-    Variant{"direct<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
-                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
-                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
-                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
-            }, true}
-
-#define GVAR(WM, WN, TM, TN, EPI, WPE, BK)                                                            \
-    Variant{"glds<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
-                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
-                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
-                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, true>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
-            }, true}
+#define RVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("regs", false, WM, WN, TM, TN, EPI, WPE, BK)
+#define GVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("glds", true, WM, WN, TM, TN, EPI, WPE, BK)
 
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
@@ -81,7 +61,7 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
     CK(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
     GemmArgs g{};
     g.A = A; g.lda = K; g.W = W; g.C = C; g.ldc = outN; g.M = M; g.N = N; g.K = K;
-    g.norm = norm; g.norm_w = w; g.eps = 1e-6f;
+    g.norm = norm; g.eps = 1e-6f;
     float *qo = nullptr, *ck = nullptr, *cv = nullptr, *rc = nullptr, *rsn = nullptr;
     if (epi == EPI_QKV) {  // stories15M attention geometry: H = KVH = 6, HD = 48, L = 256
         g.H = 6; g.KVH = 6; g.HD = 48; g.L = 256; g.Smax = 256; g.start_pos = 0;
@@ -97,20 +77,13 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
         g.C = qo;  // the correctness check reads the q section
         g.ldc = 288;
     }
-    // direct variants: W with the RMSNorm weight folded into its columns (as the runtime does)
-    float* Wf = W;
+    // W with the RMSNorm weight folded into its columns (as l3_finalize does)
     if (norm) {
         std::vector<float> hWf(hW);
         for (size_t n = 0; n < (size_t)N; ++n)
             for (size_t k = 0; k < (size_t)K; ++k) hWf[n * K + k] *= hw[k];
-        CK(hipMalloc(&Wf, hWf.size() * 4));
-        CK(hipMemcpy(Wf, hWf.data(), hWf.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(W, hWf.data(), hWf.size() * 4, hipMemcpyHostToDevice));
     }
-    auto args_for = [&](const Variant& v) {
-        GemmArgs a = g;
-        if (v.direct) a.W = Wf;
-        return a;
-    };
     hipStream_t s;
     CK(hipStreamCreate(&s));
     const double flops = 2.0 * M * N * K;
@@ -120,7 +93,7 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
     std::vector<float> ref((size_t)M * outN), got((size_t)M * outN);
     for (size_t v = 0; v < vars.size(); ++v) {
         CK(hipMemsetAsync(g.C, 0, (size_t)M * outN * 4, s));
-        vars[v].run(args_for(vars[v]), s);
+        vars[v].run(g, s);
         CK(hipGetLastError());
         CK(hipStreamSynchronize(s));
         CK(hipMemcpy(v ? got.data() : ref.data(), g.C, got.size() * 4, hipMemcpyDeviceToHost));
@@ -140,9 +113,8 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
     CK(hipEventCreate(&e1));
     for (int r = 0; r < rounds + 1; ++r) {
         for (size_t v = 0; v < vars.size(); ++v) {
-            const GemmArgs a = args_for(vars[v]);
             CK(hipEventRecord(e0, s));
-            for (int i = 0; i < iters; ++i) vars[v].run(a, s);
+            for (int i = 0; i < iters; ++i) vars[v].run(g, s);
             CK(hipEventRecord(e1, s));
             CK(hipEventSynchronize(e1));
             float ms = 0;
@@ -158,71 +130,65 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
                vars[v].name.c_str(), med, med / 157.3 * 100, x.front(), x.back(), flops / (med * 1e12) * 1e6);
     }
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(w)); CK(hipFree(C));
-    if (Wf != W) CK(hipFree(Wf));
     if (qo) { CK(hipFree(qo)); CK(hipFree(ck)); CK(hipFree(cv)); CK(hipFree(rc)); CK(hipFree(rsn)); }
     CK(hipStreamDestroy(s));
 }
 
-// Diagnostic: clock and cycle split per block from in-kernel stamps (STAMP build).
-// Per block: shader-clock (s_memtime) and 100 MHz real-time stamps at start, after the first
-// k-tile is staged (prologue), after the main loop, and at the end (epilogue).  Residency =
-// sum of block lifetimes / (launch span x 256 CUs): the average number of blocks a CU holds.
+// Diagnostic: cycle split per block from in-kernel stamps (STAMP build): shader-counter
+// (s_memtime) and 100 MHz real-time stamps at start, after the first k-tile is staged
+// (prologue), after the main loop, and after the epilogue.  Residency = sum of block lifetimes
+// / (launch span x 256 CUs): the average number of blocks a CU holds.
 template <int WM, int WN, int TM, int TN, int EPI, int WPE, int BK>
 static void stamp_report(const char* label, int M, int K, int N, bool norm) {
     const int outN = EPI == EPI_SWIGLU ? N / 2 : N;
-    float *A, *W, *w, *C;
+    float *A, *W, *C;
     CK(hipMalloc(&A, (size_t)M * K * 4)); CK(hipMalloc(&W, (size_t)N * K * 4));
-    CK(hipMalloc(&w, (size_t)K * 4)); CK(hipMalloc(&C, (size_t)M * outN * 4));
-    std::vector<float> hA((size_t)M * K), hW((size_t)N * K), hw(K, 1.0f);
+    CK(hipMalloc(&C, (size_t)M * outN * 4));
+    std::vector<float> hA((size_t)M * K), hW((size_t)N * K);
     fill(hA, -1.f, 1.f, 1); fill(hW, -0.05f, 0.05f, 2);
     CK(hipMemcpy(A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(W, hW.data(), hW.size() * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(w, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     unsigned long long* st;
-    CK(hipMalloc(&st, (size_t)tiles * 14 * 8));
+    CK(hipMalloc(&st, (size_t)tiles * 10 * 8));
     GemmArgs g{};
     g.A = A; g.lda = K; g.W = W; g.C = C; g.ldc = outN; g.M = M; g.N = N; g.K = K;
-    g.norm = norm; g.norm_w = w; g.eps = 1e-6f; g.stamps = st;
+    g.norm = norm; g.eps = 1e-6f; g.stamps = st;
     for (int it = 0; it < 20; ++it)  // back-to-back launches so the clock settles; last one kept
         hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, true, BK>), dim3(tiles), dim3(256), 0, 0, g);
     CK(hipDeviceSynchronize());
-    std::vector<unsigned long long> h((size_t)tiles * 14);
+    std::vector<unsigned long long> h((size_t)tiles * 10);
     CK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-    std::vector<double> mhz, pro, loop, epi, e_stage, e_bar, e_store;
+    std::vector<double> ratio, pro, loop, epi;
     unsigned long long t0 = ~0ull, t1 = 0;
     double life = 0;
     for (int b = 0; b < tiles; ++b) {
-        const unsigned long long* d = &h[(size_t)b * 14];
-        if (d[11] > d[1]) mhz.push_back((double)(d[10] - d[0]) / (double)(d[11] - d[1]) * 100.0);
+        const unsigned long long* d = &h[(size_t)b * 10];
+        if (d[7] > d[1]) ratio.push_back((double)(d[6] - d[0]) / (double)(d[7] - d[1]) * 100.0);
         pro.push_back((double)(d[2] - d[0]));
         loop.push_back((double)(d[4] - d[2]));
-        epi.push_back((double)(d[10] - d[4]));
-        e_stage.push_back((double)(d[6] - d[4]));
-        e_bar.push_back((double)(d[8] - d[6]));
-        e_store.push_back((double)(d[10] - d[8]));
-        life += (double)(d[11] - d[1]);
-        t0 = std::min(t0, d[1]); t1 = std::max(t1, d[11]);
+        epi.push_back((double)(d[6] - d[4]));
+        life += (double)(d[7] - d[1]);
+        t0 = std::min(t0, d[1]); t1 = std::max(t1, d[7]);
     }
     auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
     const double mfma_cycles = (double)K / 4 * TM * TN * 32;  // per wave, 16x16x4 f32 at 32 cyc
     const double span = (double)(t1 - t0);
-    printf("\n== stamps %s wpe%d bk%d: blocks %d, clock median %.0f MHz, prologue median %.0f cyc, "
-           "main loop median %.0f cyc (MFMA-only %.0f cyc per wave), epilogue median %.0f cyc, "
-           "launch span %.1f us, residency %.2f blocks/CU\n"
-           "   epilogue split (wave 0): stage %.0f, barrier %.0f, store %.0f cyc\n",
-           label, WPE, BK, tiles, med(mhz), med(pro), med(loop), mfma_cycles, med(epi), span / 100.0,
-           life / (span * 256.0), med(e_stage), med(e_bar), med(e_store));
-    CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(w)); CK(hipFree(C)); CK(hipFree(st));
+    printf("\n== stamps %s wpe%d bk%d: blocks %d, s_memtime rate %.0f MHz, prologue median %.0f, "
+           "main loop median %.0f (MFMA-only %.0f per wave), epilogue median %.0f counts; "
+           "launch span %.1f us, residency %.2f blocks/CU\n",
+           label, WPE, BK, tiles, med(ratio), med(pro), med(loop), mfma_cycles, med(epi), span / 100.0,
+           life / (span * 256.0));
+    CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(C)); CK(hipFree(st));
 }
 
 int main(int argc, char** argv) {
     if (argc > 3 && std::string(argv[3]) == "stamps") {
-        stamp_report<2, 2, 4, 4, EPI_SWIGLU, 2, 16>("gate|up 128x128", 65536, 288, 1536, true);
         stamp_report<2, 2, 4, 4, EPI_SWIGLU, 3, 16>("gate|up 128x128", 65536, 288, 1536, true);
+        stamp_report<2, 2, 4, 3, EPI_STORE, 4, 16>("QKV-shape 128x96", 65536, 288, 864, true);
         stamp_report<2, 2, 4, 3, EPI_RESID, 2, 32>("down 128x96", 65536, 768, 288, false);
-        stamp_report<2, 2, 2, 3, EPI_RESID, 2, 32>("O-proj 64x96", 65536, 288, 288, false);
+        stamp_report<2, 2, 2, 3, EPI_RESID, 3, 32>("O-proj 64x96", 65536, 288, 288, false);
         return 0;
     }
     const int rounds = argc > 1 ? atoi(argv[1]) : 5;
@@ -231,22 +197,22 @@ int main(int argc, char** argv) {
     const bool c5 = argc > 3 && std::string(argv[3]) == "c5";
     if (!c5) {
     run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
-              {DVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
+              {RVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
                GVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, iters);
     run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
-              {DVAR(2, 2, 4, 4, EPI_QKV, 3, 16), GVAR(2, 2, 4, 4, EPI_QKV, 3, 16),
+              {RVAR(2, 2, 4, 4, EPI_QKV, 3, 16), GVAR(2, 2, 4, 4, EPI_QKV, 3, 16),
                GVAR(2, 2, 4, 3, EPI_QKV, 3, 16), GVAR(2, 2, 4, 3, EPI_QKV, 4, 16)}, rounds, iters);
     run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
-              {DVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(2, 2, 4, 3, EPI_RESID, 2, 32),
-               GVAR(2, 2, 4, 3, EPI_RESID, 3, 32), GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
+              {RVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(2, 2, 4, 3, EPI_RESID, 2, 32),
+               GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
     run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
-              {DVAR(2, 2, 2, 3, EPI_RESID, 2, 32), GVAR(2, 2, 2, 3, EPI_RESID, 3, 32),
+              {RVAR(2, 2, 2, 3, EPI_RESID, 2, 32), GVAR(2, 2, 2, 3, EPI_RESID, 3, 32),
                GVAR(2, 2, 2, 3, EPI_RESID, 3, 16), GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
     } else {
     // Llama-3-8B shapes (C5) at M = 16384 rows (tuning size)
     const int Mc = 16384;
     run_shape("C5 gate|up", EPI_SWIGLU, Mc, 4096, 28672, true,
-              {DVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
+              {RVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
                GVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, 3);
     run_shape("C5 QKV-shape (store)", EPI_STORE, Mc, 4096, 6144, true,
               {GVAR(2, 2, 4, 4, EPI_STORE, 3, 16), GVAR(2, 2, 4, 3, EPI_STORE, 4, 16),
