@@ -64,8 +64,67 @@ __device__ __forceinline__ int lds_swz(int r) {
     return BK == 16 ? (r >> 1) & 3 : r & 7;
 }
 
-// Register-direct epilogue.  The MFMA operands are swapped (W fragment as
-// the A operand, activation fragment as B), so the accumulator of tile (i, j) is C^T: lane l
+// QKV epilogue (same register-direct fragment map as direct_epilogue): RMSNorm row factor,
+// RoPE on the two (even, odd) pairs of each float4 (llama3.py:41-76), then q (scaled) to the q
+// buffer, k / v appended to the KV cache (llama3.py:184-185).  Branch-free over the q/k/v
+// sections (a V tile rotates by cos = 1, sin = 0, which is exact), and every RoPE table load is
+// issued before the first store: a load's vmcnt wait also waits for all older stores.
+template <int TM, int TN>
+__device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&acc)[TM][TN],
+                                             const float (&rs)[TM], int mrow0, int ncol0,
+                                             int lane) {
+    const int frow = lane & 15, fq4 = 4 * (lane >> 4);
+    const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD, hd2 = p.HD >> 1;
+    const int sp = start_of(p);
+    int rowc[TM], bidx[TM], pos[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        rowc[i] = min(mrow0 + i * 16 + frow, p.M - 1);
+        bidx[i] = rowc[i] / p.L;
+        pos[i] = sp + rowc[i] - bidx[i] * p.L;
+    }
+    int sec[TN], head[TN], d[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = min(ncol0 + j * 16 + fq4, p.N - 4);
+        sec[j] = col < qdim ? 0 : (col < qdim + kvdim ? 1 : 2);
+        const int cc = col - (sec[j] == 0 ? 0 : (sec[j] == 1 ? qdim : qdim + kvdim));
+        head[j] = cc / p.HD;
+        d[j] = cc - head[j] * p.HD;
+    }
+    float2 cs[TM][TN], sn[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int t = pos[i] * hd2 + (d[j] >> 1);
+            cs[i][j] = *reinterpret_cast<const float2*>(p.rope_cos + t);
+            sn[i][j] = *reinterpret_cast<const float2*>(p.rope_sin + t);
+        }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int row = mrow0 + i * 16 + frow;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = ncol0 + j * 16 + fq4;
+            if (row >= p.M || col >= p.N) continue;
+            const bool rot = sec[j] < 2;
+            const float2 c = rot ? cs[i][j] : float2{1.f, 1.f};
+            const float2 s = rot ? sn[i][j] : float2{0.f, 0.f};
+            const f32x4 v = acc[i][j] * (sec[j] == 0 ? rs[i] * p.q_scale : rs[i]);
+            const f32x4 r = {v.x * c.x - v.y * s.x, v.x * s.x + v.y * c.x,
+                             v.z * c.y - v.w * s.y, v.z * s.y + v.w * c.y};
+            float* base = sec[j] == 0 ? p.q_out : (sec[j] == 1 ? p.cache_k : p.cache_v);
+            const int64_t off = sec[j] == 0
+                                    ? (int64_t)row * qdim + col
+                                    : (((int64_t)bidx[i] * p.KVH + head[j]) * p.Smax + pos[i]) * p.HD + d[j];
+            *reinterpret_cast<f32x4*>(base + off) = r;
+        }
+    }
+}
+
+// Register-direct epilogue (EPI_STORE / EPI_RESID / EPI_SWIGLU).  The MFMA operands are swapped
+// (W fragment as the A operand, activation fragment as B), so the accumulator of tile (i, j) is C^T: lane l
 // holds C[row = 16i + (l&15)][col = 16j + 4(l>>4) + r], r = 0..3 — four consecutive columns
 // of one row, i.e. one 16-byte store, with no LDS staging and no block barrier.  rs[i] is the
 // lane's RMSNorm factor for its row of tile i (1 without norm); res the prefetched residual.
@@ -96,38 +155,14 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
                 const int col = ncol0 + j * 16 + fq4;
                 if (col >= p.N) continue;
                 f32x4 v = acc[i][j];
-                if constexpr (EPI == EPI_QKV) {
-                    v *= sc;
-                    // RoPE on the two (even, odd) pairs of the float4 (llama3.py:41-76), then
-                    // q scaling / KV-cache append (llama3.py:184-185)
-                    const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
-                    const int bidx = row / p.L, pos = start_of(p) + row - bidx * p.L;
-                    const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
-                    const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
-                    const int head = cc / p.HD, d = cc - head * p.HD;
-                    if (is_q || is_k) {
-                        const int t = pos * (p.HD >> 1) + (d >> 1);
-                        const float2 c = *reinterpret_cast<const float2*>(p.rope_cos + t);
-                        const float2 sn = *reinterpret_cast<const float2*>(p.rope_sin + t);
-                        v = f32x4{v.x * c.x - v.y * sn.x, v.x * sn.x + v.y * c.x,
-                                  v.z * c.y - v.w * sn.y, v.z * sn.y + v.w * c.y};
-                    }
-                    if (is_q) {
-                        *reinterpret_cast<f32x4*>(p.q_out + (int64_t)row * qdim + col) = v * p.q_scale;
-                    } else {
-                        float* cache = is_k ? p.cache_k : p.cache_v;
-                        *reinterpret_cast<f32x4*>(cache + (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d) = v;
-                    }
+                float* dst = p.C + (int64_t)row * p.ldc + col;
+                if constexpr (EPI == EPI_RESID) {
+                    if constexpr (RES_PREFETCH) v += res[i * TN + j];
+                    else v += *reinterpret_cast<const f32x4*>(dst);
                 } else {
-                    float* dst = p.C + (int64_t)row * p.ldc + col;
-                    if constexpr (EPI == EPI_RESID) {
-                        if constexpr (RES_PREFETCH) v += res[i * TN + j];
-                        else v += *reinterpret_cast<const f32x4*>(dst);
-                    } else {
-                        v *= sc;
-                    }
-                    *reinterpret_cast<f32x4*>(dst) = v;
+                    v *= sc;
                 }
+                *reinterpret_cast<f32x4*>(dst) = v;
             }
         }
     }
@@ -323,7 +358,8 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         rs[i] = p.norm ? 1.0f / sqrtf(v * inv_k + p.eps) : 1.0f;
     }
     L3_STAMP(2);
-    direct_epilogue<TM, TN, EPI, RES_PREFETCH>(p, acc, rs, res, m0 + arow0, n0 + brow0, lane);
+    if constexpr (EPI == EPI_QKV) qkv_epilogue<TM, TN>(p, acc, rs, m0 + arow0, n0 + brow0, lane);
+    else direct_epilogue<TM, TN, EPI, RES_PREFETCH>(p, acc, rs, res, m0 + arow0, n0 + brow0, lane);
     L3_STAMP(3);
     if constexpr (STAMP) {
         if (tid == 0) {
