@@ -129,6 +129,9 @@ int l3_attention_forward_host(l3_ctx* ctx, int32_t layer, const float* x_host, i
 /* ---- op-level entry points (reference module functions and classes) ------ */
 /* softmax over the last axis (llama3.py:22-24); rows x n. */
 int l3_op_softmax_host(l3_ctx* ctx, const float* x, int64_t rows, int64_t n, float* y);
+/* argmax over the last axis with np.argmax's tie-break: first index of the maximum, the first
+ * NaN if any (llama3.py:320); rows x n -> rows int32. */
+int l3_op_argmax_host(l3_ctx* ctx, const float* x, int64_t rows, int64_t n, int32_t* out);
 /* silu (llama3.py:27-28); n elements. */
 int l3_op_silu_host(l3_ctx* ctx, const float* x, int64_t n, float* y);
 /* RMSNorm (llama3.py:111-114); rows x dim. */

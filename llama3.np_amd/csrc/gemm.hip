@@ -16,17 +16,30 @@ static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+template <int EPI, int MR, int LPU>
+static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
+    const int units = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? a.N / 2 : a.N;
+    const int per_block = 4 * (64 / LPU);
+    const dim3 grid((unsigned)((units + per_block - 1) / per_block)), block(256);
+    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU>), grid, block, (size_t)MR * a.K * 4, s, a);
+    return hipGetLastError();
+}
+
+// lanes per unit from K: ~5-8 float4 per lane per W row in one chunk at the stories15M sizes
+template <int EPI, int MR>
+static hipError_t launch_gemv_mr(const GemmArgs& a, hipStream_t s) {
+    const int k4 = a.K / 4;
+    if (k4 <= 128) return launch_gemv_lpu<EPI, MR, 16>(a, s);
+    if (k4 <= 256) return launch_gemv_lpu<EPI, MR, 32>(a, s);
+    return launch_gemv_lpu<EPI, MR, 64>(a, s);
+}
+
 template <int EPI>
 static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
-    const int units = EPI == EPI_SWIGLU ? a.N / 2 : a.N;
-    const dim3 grid((unsigned)((units + 63) / 64)), block(256);
-    const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
-    const size_t lds = ((size_t)mr * a.K + 8) * 4;  // staged A rows + row sums
-    if (mr == 1) hipLaunchKernelGGL((gemv_kernel<EPI, 1>), grid, block, lds, s, a);
-    else if (mr == 2) hipLaunchKernelGGL((gemv_kernel<EPI, 2>), grid, block, lds, s, a);
-    else if (mr == 4) hipLaunchKernelGGL((gemv_kernel<EPI, 4>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((gemv_kernel<EPI, 8>), grid, block, lds, s, a);
-    return hipGetLastError();
+    if (a.M <= 1) return launch_gemv_mr<EPI, 1>(a, s);
+    if (a.M <= 2) return launch_gemv_mr<EPI, 2>(a, s);
+    if (a.M <= 4) return launch_gemv_mr<EPI, 4>(a, s);
+    return launch_gemv_mr<EPI, 8>(a, s);
 }
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
@@ -36,7 +49,7 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.N % 4 != 0 || a.ldc % 4 != 0 || a.lda % 4 != 0) return hipErrorInvalidValue;  // 16-B rows
     // M <= 8 (decode, short prompts): weight-streaming GEMV with the same epilogues
     const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
-    if (a.M <= 8 && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS
+    if (a.M <= 8 && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS (QKV: N even)
         switch (epi) {
             case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);
             case EPI_QKV: return launch_gemv<EPI_QKV>(a, s);

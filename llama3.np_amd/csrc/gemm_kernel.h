@@ -376,71 +376,74 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 #undef L3_STAMP
 
 // ---------------------------------------------------------------------------------------
-// Skinny GEMM for M <= 8 rows (greedy decode, short prompts): the op is weight-streaming
-// (HBM / latency bound), so no LDS tiles and no MFMA.  A block (4 waves) stages the A rows
-// (times the RMSNorm weight) in LDS once; each wave owns 16 output units (a unit = one W row,
-// or a gate/up row pair for SwiGLU); lane (c = lane&15, kq = lane>>4) streams 16-byte pieces
-// k = 16i + 4kq of its unit's W row(s) straight to registers (all loads of a chunk issued
-// before the first use), the four k-quarters are summed with two shuffles, and lanes 0-15 run
-// the same epilogues as the tiled kernel.
-template <int EPI, int MR>
+// Skinny GEMM for M <= 8 rows (greedy decode, short prompts): weight-streaming, HBM / latency
+// bound, so no MFMA.  A unit is one W row (EPI_STORE / EPI_RESID), a RoPE pair (EPI_QKV: rows
+// 2u, 2u + 1) or a gate/up pair (EPI_SWIGLU: fused rows 32(u/16) + u%16 and + 16).  LPU lanes
+// share a unit and split its K: lane j streams float4 k4 = j + LPU t, with a whole chunk of CH
+// loads per row in flight before the first FMA (one memory round trip per chunk, not one per
+// load), and a butterfly over the LPU lanes completes the dot products.  The M input rows are
+// staged in LDS once per block; the RMSNorm sum of squares comes from the same lane-split reads
+// (the norm weight itself is folded into W, launch_fold_cols).
+template <int EPI, int MR, int LPU>
 __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
-    extern __shared__ __attribute__((aligned(16))) float xs[];  // [MR][K] then row sums [MR]
-    float* rsum = xs + MR * p.K;
+    extern __shared__ __attribute__((aligned(16))) float xs[];  // [MR][K]
+    constexpr int ROWS = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? 2 : 1;
+    constexpr int UPW = 64 / LPU;  // units per wave
+    constexpr int CH = 8;          // float4 per W row per lane in flight
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int K4 = p.K / 4;
-    if (tid < MR) rsum[tid] = 0.f;
-    __syncthreads();
-    for (int f = tid; f < p.M * K4; f += 256) {
-        const int m = f / K4, k = (f - m * K4) * 4;
-        f32x4 v = *reinterpret_cast<const f32x4*>(p.A + (int64_t)m * p.lda + k);
-        if (p.norm) {
-            atomicAdd(&rsum[m], v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
-            // the norm weight itself is folded into W (launch_fold_cols)
+    const int K4 = p.K >> 2;
+    const int j = lane % LPU;
+    const int unit = (blockIdx.x * 4 + wid) * UPW + lane / LPU;
+    const int nunits = ROWS == 2 ? p.N / 2 : p.N;
+    const bool valid = unit < nunits;
+    const int u = valid ? unit : 0;
+    int wrow[ROWS];
+    if constexpr (EPI == EPI_SWIGLU) {
+        wrow[0] = 32 * (u / 16) + (u % 16);
+        wrow[ROWS - 1] = wrow[0] + 16;
+    } else if constexpr (EPI == EPI_QKV) {
+        wrow[0] = 2 * u;
+        wrow[ROWS - 1] = 2 * u + 1;
+    } else {
+        wrow[0] = u;
+    }
+    const f32x4* W4 = reinterpret_cast<const f32x4*>(p.W);
+    f32x4 w[ROWS][CH];
+    auto load_chunk = [&](int t0) {
+#pragma unroll
+        for (int t = 0; t < CH; ++t) {
+            const int k4 = j + LPU * (t0 + t);
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r)
+                w[r][t] = k4 < K4 ? W4[(int64_t)wrow[r] * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
         }
-        *reinterpret_cast<f32x4*>(xs + m * p.K + k) = v;
+    };
+    load_chunk(0);  // in flight while the input rows are staged
+    for (int f = tid; f < p.M * K4; f += 256) {
+        const int m = f / K4, k4 = f - m * K4;
+        reinterpret_cast<f32x4*>(xs)[f] = reinterpret_cast<const f32x4*>(p.A + (int64_t)m * p.lda)[k4];
     }
     __syncthreads();
 
-    constexpr int ROWS = EPI == EPI_SWIGLU ? 2 : 1;   // W rows per unit
-    const int c = lane & 15, kq = lane >> 4;
-    const int unit = (blockIdx.x * 4 + wid) * 16 + c;
-    const int nunits = EPI == EPI_SWIGLU ? p.N / 2 : p.N;
-    // W row(s) of this unit: SwiGLU unit u = hidden column u -> fused rows 32(u/16) + u%16 (+16)
-    int wrow[ROWS];
-    if constexpr (EPI == EPI_SWIGLU) {
-        wrow[0] = 32 * (unit / 16) + (unit % 16);
-        wrow[ROWS - 1] = wrow[0] + 16;
-    } else {
-        wrow[0] = unit;
+    float acc[ROWS][MR], ss[MR];
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+        ss[m] = 0.f;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r][m] = 0.f;
     }
-    const bool valid = unit < nunits;
-    float acc[ROWS][MR];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r)
-#pragma unroll
-        for (int m = 0; m < MR; ++m) acc[r][m] = 0.f;
-    constexpr int CH = 8;  // 16-byte pieces in flight per W row per lane
-    const int nk = p.K / 16;
-    for (int i0 = 0; i0 < nk; i0 += CH) {
-        f32x4 w[ROWS][CH];
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r)
-#pragma unroll
-            for (int t = 0; t < CH; ++t) {
-                const int k = (i0 + t) * 16 + 4 * kq;
-                w[r][t] = (valid && i0 + t < nk)
-                              ? *reinterpret_cast<const f32x4*>(p.W + (int64_t)wrow[r] * p.K + k)
-                              : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+    const int nt = (K4 + LPU - 1) / LPU;
+    for (int t0 = 0; t0 < nt; t0 += CH) {
+        if (t0) load_chunk(t0);
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
-            const int k = (i0 + t) * 16 + 4 * kq;
-            if (i0 + t >= nk) break;
+            const int k4 = j + LPU * (t0 + t);
+            if (k4 >= K4) break;
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 if (m >= p.M) break;
-                const f32x4 x = *reinterpret_cast<const f32x4*>(xs + m * p.K + k);
+                const f32x4 x = reinterpret_cast<const f32x4*>(xs + m * p.K)[k4];
+                ss[m] += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r)
                     acc[r][m] += w[r][t].x * x.x + w[r][t].y * x.y + w[r][t].z * x.z + w[r][t].w * x.w;
@@ -448,35 +451,39 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
         }
     }
 #pragma unroll
-    for (int r = 0; r < ROWS; ++r)
+    for (int o = LPU / 2; o > 0; o >>= 1)
 #pragma unroll
         for (int m = 0; m < MR; ++m) {
-            acc[r][m] += __shfl_xor(acc[r][m], 16);
-            acc[r][m] += __shfl_xor(acc[r][m], 32);
+            ss[m] += __shfl_xor(ss[m], o);
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) acc[r][m] += __shfl_xor(acc[r][m], o);
         }
+    if (j != 0 || !valid) return;
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
         if (m >= p.M) break;
-        const float sc = p.norm ? 1.0f / sqrtf(rsum[m] / (float)p.K + p.eps) : 1.0f;
+        const float sc = p.norm ? 1.0f / sqrtf(ss[m] / (float)p.K + p.eps) : 1.0f;
         if constexpr (EPI == EPI_QKV) {
+            // columns 2u, 2u + 1: one RoPE pair (llama3.py:41-76), then q / KV-cache append
             const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
-            const int col = unit;
-            float v = acc[0][m] * sc;
-            const float partner = __shfl_xor(v, 1);  // RoPE pair partner: lane c ^ 1
-            if (kq == 0 && valid) {
-                const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
-                const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
-                const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
-                const int head = cc / p.HD, d = cc - head * p.HD;
-                if (is_q || is_k) {
-                    const int t = pos * (p.HD >> 1) + (d >> 1);
-                    const float cs = p.rope_cos[t], sn = p.rope_sin[t];
-                    v = (d & 1) ? (partner * sn + v * cs) : (v * cs - partner * sn);
-                }
-                if (is_q) p.q_out[(int64_t)m * qdim + col] = v * p.q_scale;
-                else (is_k ? p.cache_k : p.cache_v)[(((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d] = v;
+            const int col = 2 * unit;
+            float v0 = acc[0][m] * sc, v1 = acc[ROWS - 1][m] * sc;
+            const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
+            const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
+            const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
+            const int head = cc / p.HD, d = cc - head * p.HD;
+            if (is_q || is_k) {
+                const int t = pos * (p.HD >> 1) + (d >> 1);
+                const float cs = p.rope_cos[t], sn = p.rope_sin[t];
+                const float r0 = v0 * cs - v1 * sn, r1 = v0 * sn + v1 * cs;
+                v0 = r0;
+                v1 = r1;
             }
-        } else if (kq == 0 && valid) {
+            float2* dst = is_q ? reinterpret_cast<float2*>(p.q_out + (int64_t)m * qdim + col)
+                               : reinterpret_cast<float2*>((is_k ? p.cache_k : p.cache_v) +
+                                                           (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d);
+            *dst = is_q ? float2{v0 * p.q_scale, v1 * p.q_scale} : float2{v0, v1};
+        } else {
             float* dst = p.C + (int64_t)m * p.ldc + unit;
             if constexpr (EPI == EPI_SWIGLU) *dst = silu_f(acc[0][m] * sc) * (acc[ROWS - 1][m] * sc);
             else if constexpr (EPI == EPI_RESID) *dst += acc[0][m];

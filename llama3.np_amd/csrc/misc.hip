@@ -30,40 +30,71 @@ __global__ void embed_kernel(const int32_t* __restrict__ ids, const float* __res
     }
 }
 
-// argmax over each row with np.argmax's first-index tie-break (llama3.py:320).
-__global__ void argmax_kernel(const float* __restrict__ x, int n, int32_t* __restrict__ out,
-                              int* __restrict__ pos_dev) {
+// argmax over each row with np.argmax's first-index tie-break (llama3.py:320); a NaN wins
+// (np.argmax returns the first NaN).  One 1024-thread block per row: each thread has all of
+// its float4 loads in flight at once (8 per thread at the 32000-wide vocab), then a wavefront
+// butterfly and a 16-way LDS step — a decode step waits on one memory round trip, not on a
+// serial walk of the row.
+__device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi) {
+    const bool vn = v != v, bn = bv != bv;
+    if (vn || bn) return vn && (!bn || i < bi);
+    return v > bv || (v == bv && i < bi);
+}
+
+__global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ x, int n,
+                                                      int32_t* __restrict__ out,
+                                                      int* __restrict__ pos_dev) {
+    constexpr int NT = 1024, U = 8;
     const float* row = x + (int64_t)blockIdx.x * n;
+    const int tid = threadIdx.x;
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const float v = row[i];
-        if (v > best || (v == best && i < bi) || (v != v && best == best)) { best = v; bi = i; }
-    }
-    __shared__ float sv[256];
-    __shared__ int si[256];
-    sv[threadIdx.x] = best;
-    si[threadIdx.x] = bi;
-    __syncthreads();
-    for (int st = 128; st > 0; st >>= 1) {
-        if (threadIdx.x < st) {
-            const float ov = sv[threadIdx.x + st];
-            const int oi = si[threadIdx.x + st];
-            const float cv = sv[threadIdx.x];
-            const int ci = si[threadIdx.x];
-            // NaN wins (np.argmax returns the first NaN), then larger value, then lower index
-            const bool onan = ov != ov, cnan = cv != cv;
-            bool take;
-            if (onan || cnan) take = onan && (!cnan || oi < ci);
-            else take = ov > cv || (ov == cv && oi < ci);
-            if (take) { sv[threadIdx.x] = ov; si[threadIdx.x] = oi; }
+    if ((n & 3) == 0) {  // 16-byte rows
+        const int n4 = n >> 2;
+        for (int base = 0; base < n4; base += NT * U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int f = base + u * NT + tid;
+                v[u] = f < n4 ? reinterpret_cast<const f32x4*>(row)[f] : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int f = base + u * NT + tid;
+                if (f < n4)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (argmax_better(v[u][r], 4 * f + r, best, bi)) { best = v[u][r]; bi = 4 * f + r; }
+            }
         }
-        __syncthreads();
+    } else {
+        for (int i = tid; i < n; i += NT)
+            if (argmax_better(row[i], i, best, bi)) { best = row[i]; bi = i; }
     }
-    if (threadIdx.x == 0) {
-        out[blockIdx.x] = si[0];
-        // captured decode step: the next step runs one position later (llama3.py:312-318)
-        if (pos_dev && blockIdx.x == 0) *pos_dev += 1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+    }
+    __shared__ float sv[NT / 64];
+    __shared__ int si[NT / 64];
+    if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
+    __syncthreads();
+    if (tid < 64) {
+        best = tid < NT / 64 ? sv[tid] : -INFINITY;
+        bi = tid < NT / 64 ? si[tid] : 0x7fffffff;
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) {
+            const float ov = __shfl_xor(best, o);
+            const int oi = __shfl_xor(bi, o);
+            if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+        }
+        if (tid == 0) {
+            out[blockIdx.x] = bi;
+            // captured decode step: the next step runs one position later (llama3.py:312-318)
+            if (pos_dev && blockIdx.x == 0) *pos_dev += 1;
+        }
     }
 }
 
@@ -142,7 +173,7 @@ hipError_t launch_embed(const int32_t* ids, const float* emb, float* h, int64_t 
 
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
                          int* pos_dev) {
-    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(256), 0, s, logits, n, out, pos_dev);
+    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(1024), 0, s, logits, n, out, pos_dev);
     return hipGetLastError();
 }
 

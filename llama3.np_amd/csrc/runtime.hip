@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -597,7 +598,10 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
                                hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
-    if (L == 1 && start_pos + 1 < c->d.max_seq_len) {
+    // L3_DECODE_GRAPH=0 keeps every step eager (rocprofv3 kernel tracing does not survive
+    // stream capture in this ROCm build)
+    static const bool graphs = [] { const char* e = getenv("L3_DECODE_GRAPH"); return !e || e[0] != '0'; }();
+    if (graphs && L == 1 && start_pos + 1 < c->d.max_seq_len) {
         // arm the device state for the next decode step (one position later) and capture
         const int next = start_pos + 1;
         HIP_TRY(hipMemcpy(c->dec_pos, &next, sizeof(int), hipMemcpyHostToDevice));
@@ -742,6 +746,20 @@ extern "C" int l3_op_softmax_host(l3_ctx* c, const float* x, int64_t rows, int64
     H2D(dx, x, rows * n);
     HIP_TRY(launch_softmax(dx, dy, rows, (int)n, c->stream));
     D2H(y, dy, rows * n);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_op_argmax_host(l3_ctx* c, const float* x, int64_t rows, int64_t n, int32_t* out) {
+    CHECK_CTX(c);
+    if (rows <= 0 || n <= 0 || n > INT32_MAX) return fail("argmax: bad shape %lld x %lld", (long long)rows, (long long)n);
+    if (set_dev(c)) return 1;
+    Scratch S{c};
+    SCRATCH(dx, rows * n);
+    SCRATCH(di, rows);
+    H2D(dx, x, rows * n);
+    HIP_TRY(launch_argmax(dx, rows, (int)n, reinterpret_cast<int32_t*>(di), c->stream));
+    D2H(out, di, rows);
     HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
 }

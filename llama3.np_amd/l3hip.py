@@ -60,6 +60,7 @@ _SIGNATURES = {
     "l3_greedy_generate_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
     "l3_attention_forward_host": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P]),
     "l3_op_softmax_host": (ctypes.c_int, [_P, _P, _I64, _I64, _P]),
+    "l3_op_argmax_host": (ctypes.c_int, [_P, _P, _I64, _I64, _P]),
     "l3_op_silu_host": (ctypes.c_int, [_P, _P, _I64, _P]),
     "l3_op_rmsnorm_host": (ctypes.c_int, [_P, _P, _P, _I64, _I64, _F, _P]),
     "l3_op_rope_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, _P, _P, _P]),
@@ -264,6 +265,14 @@ class Context:
         n = x.shape[-1]
         check(lib().l3_op_softmax_host(self._h, ptr(x), x.size // n, n, ptr(y)))
         return y
+
+    def op_argmax(self, x: np.ndarray) -> np.ndarray:
+        """argmax over the last axis (np.argmax tie-break, NaN first); int32 of x.shape[:-1]."""
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        n = x.shape[-1]
+        out = np.empty(x.shape[:-1], np.int32)
+        check(lib().l3_op_argmax_host(self._h, ptr(x), x.size // n, n, ptr(out)))
+        return out
 
     def op_silu(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float32)

@@ -62,6 +62,27 @@ def test_linear_integer_exact(ctx):
     np.testing.assert_array_equal(ctx.op_linear(x, w), x @ w.T)
 
 
+# ---- greedy argmax (llama3.py:320: np.argmax, first index of the max, first NaN) --------
+
+@pytest.mark.parametrize("rows,n", [(1, 32000), (3, 32000), (2, 7), (1, 1), (2, 40001), (5, 128256)])
+def test_argmax_matches_numpy(ctx, rows, n):
+    rng = np.random.default_rng(rows * 31 + n)
+    x = rng.standard_normal((rows, n)).astype(np.float32)
+    np.testing.assert_array_equal(ctx.op_argmax(x), np.argmax(x, axis=-1))
+
+
+def test_argmax_ties_nan_inf(ctx):
+    n = 32000
+    x = np.zeros((6, n), np.float32)
+    x[0, [5, 17, 31999]] = 3.0                     # ties -> first index
+    x[1, :] = -np.inf                              # all -inf -> 0
+    x[2, [40, 9000]] = np.nan; x[2, 3] = np.inf    # first NaN wins over +inf
+    x[3, 12345] = np.inf; x[3, 20000] = np.inf     # first +inf
+    x[4, :] = 1.0                                  # constant row -> 0
+    x[5, 31999] = 1e-30                            # last element strictly largest
+    np.testing.assert_array_equal(ctx.op_argmax(x), np.argmax(x, axis=-1))
+
+
 # ---- op-level module functions vs the reference's own outputs ---------------------------
 
 def test_ops_against_golden(ctx):

@@ -21,6 +21,9 @@ import synth  # noqa: E402
 
 
 def main():
+    eager = "--eager" in sys.argv  # profiling: every step eager, no device-loop leg
+    if eager:
+        os.environ["L3_DECODE_GRAPH"] = "0"
     g = np.load(os.path.join(REPO, "tests", "golden", "stories15m_default.npz"))
     args = synth.stories15m(1)
     w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=int(g["seed"]), preset="default")
@@ -38,6 +41,10 @@ def main():
     exact = ids == g["dream_ids"][0].tolist()
     t = float(np.median(runs))
     count = prompt.shape[1] + len(ids)
+    if eager:
+        print(json.dumps({"workload": "stories15M greedy decode B=1 (eager, L3_DECODE_GRAPH=0)",
+                          "ms_per_step": round(t / len(ids) * 1e3, 3), "ids_exact_vs_reference": exact}))
+        return
     # device-side loop (Llama.generate_all: graph replays back to back, one copy-back)
     dev = []
     for _ in range(3):
