@@ -29,9 +29,26 @@ static hipError_t launch_hd(const AttnArgs& a, hipStream_t s) {
     return launch_g<HD, KT, QBIG, 1>(a, s);
 }
 
+template <int HD>
+static hipError_t launch_decode(const AttnArgs& a, hipStream_t s) {
+    constexpr int R = 256 / (HD / 4);
+    const size_t lds = ((size_t)R * HD + a.Smax) * 4;
+    hipLaunchKernelGGL((attn_decode_kernel<HD>), dim3(a.H, a.B), dim3(256), lds, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (a.B <= 0 || a.L <= 0) return hipSuccess;
     if (a.KVH <= 0 || a.H % a.KVH != 0) return hipErrorInvalidValue;
+    if (a.L == 1 && a.Smax <= 8192) {  // decode: one query per (b, h)
+        switch (a.HD) {
+            case 16: return launch_decode<16>(a, s);
+            case 48: return launch_decode<48>(a, s);
+            case 64: return launch_decode<64>(a, s);
+            case 128: return launch_decode<128>(a, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (a.HD) {
         case 16: return launch_hd<16, 64, 4>(a, s);
         case 48: return launch_hd<48, 64, 4>(a, s);

@@ -298,4 +298,87 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Decode attention (L = 1: one query per (batch, head) at position pos attends keys [0, pos],
+// no mask, llama3.py:186-210 with the cache slice :186-187).  A workgroup owns one (b, h);
+// the work is three short memory-bound passes, so the kernel is built around round trips, not
+// MFMA: (1) scores, one key per thread (its HD/4 float4 loads in flight together), kept in
+// LDS; (2) block max and exp2 / sum; (3) P.V with rg = tid / (HD/4) key groups x HD/4 float4
+// columns, the first VP rows of each thread's V prefetched at kernel entry so their latency
+// hides under passes 1-2; partial O reduced through LDS.  q is pre-scaled by log2(e)/sqrt(HD).
+template <int HD>
+__global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
+    constexpr int D4 = HD / 4, R = 256 / D4, VP = 8;
+    extern __shared__ __attribute__((aligned(16))) float dsm[];  // [R][HD] partials, [Smax] scores
+    float* red = dsm;
+    float* sc = dsm + R * HD;
+    __shared__ float wred[8];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int kvh = h / (p.H / p.KVH);
+    const int pos = start_of(p);
+    const int S = pos + 1;
+    const int64_t kv_base = ((int64_t)b * p.KVH + kvh) * p.Smax * HD;
+    const f32x4* K4 = reinterpret_cast<const f32x4*>(p.cache_k + kv_base);
+    const f32x4* V4 = reinterpret_cast<const f32x4*>(p.cache_v + kv_base);
+    const int rg = tid / D4, d4 = tid - rg * D4;
+    f32x4 vpre[VP];
+#pragma unroll
+    for (int t = 0; t < VP; ++t) {
+        const int k = rg + t * R;
+        vpre[t] = (rg < R && k < S) ? V4[(int64_t)k * D4 + d4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const f32x4* q4 = reinterpret_cast<const f32x4*>(p.q + ((int64_t)b * p.H + h) * HD);
+    f32x4 q[D4];
+#pragma unroll
+    for (int i = 0; i < D4; ++i) q[i] = q4[i];
+
+    // (1) scores
+    float m = -INFINITY;
+    for (int k = tid; k < S; k += 256) {
+        f32x4 kv[D4];
+#pragma unroll
+        for (int i = 0; i < D4; ++i) kv[i] = K4[(int64_t)k * D4 + i];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < D4; ++i) s += kv[i].x * q[i].x + kv[i].y * q[i].y + kv[i].z * q[i].z + kv[i].w * q[i].w;
+        sc[k] = s;
+        m = fmaxf(m, s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) wred[wid] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
+    // (2) p = exp2(s - max), row sum
+    float l = 0.f;
+    for (int k = tid; k < S; k += 256) {
+        const float e = __builtin_amdgcn_exp2f(sc[k] - m);
+        sc[k] = e;
+        l += e;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+    if (lane == 0) wred[4 + wid] = l;
+    __syncthreads();  // p complete in LDS; row sum in wred[4..7]
+    l = (wred[4] + wred[5]) + (wred[6] + wred[7]);
+    // (3) P.V
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (rg < R) {
+#pragma unroll
+        for (int t = 0; t < VP; ++t) {
+            const int k = rg + t * R;
+            if (k < S) acc += sc[k] * vpre[t];
+        }
+        for (int k = rg + VP * R; k < S; k += R) acc += sc[k] * V4[(int64_t)k * D4 + d4];
+        reinterpret_cast<f32x4*>(red)[rg * D4 + d4] = acc;
+    }
+    __syncthreads();
+    if (tid < D4) {
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < R; ++r) o += reinterpret_cast<const f32x4*>(red)[r * D4 + tid];
+        reinterpret_cast<f32x4*>(p.out + ((int64_t)b * p.H + h) * HD)[tid] = o * (1.0f / l);
+    }
+}
+
 }  // namespace l3
