@@ -290,3 +290,31 @@ def test_generate_all_batched_matches_oracle(tmpdir_mod):
             got = m.generate_all(prompt, n)
             assert got.dtype == np.int64 and got.shape == (shape[0], n - shape[1])
             np.testing.assert_array_equal(got, orc.greedy_ids(ref, prompt, n))
+
+
+def test_llama3_head_dim_gqa_decode_with_norm_weights(tmpdir_mod):
+    """Llama-3 head geometry (HD = 128, n_rep = 4) with non-unit RMSNorm weights (exercises the
+    fold into W): prefill at B = 8 (the widest GEMV row block), then five L = 1 decode steps
+    (decode attention, GEMV epilogues) fed the oracle's own ids, logits compared every step."""
+    from config import ModelArgs
+
+    args = ModelArgs(dim=512, n_layers=2, n_heads=4, n_kv_heads=1, vocab_size=1000,
+                     max_seq_len=96, max_batch_size=8)
+    w = synth.make_weights(args, 1024, seed=11, preset="sharp")
+    rng = np.random.default_rng(12)
+    for k in list(w):
+        if k.endswith("norm.weight") or k.endswith("layernorm.weight"):
+            w[k] = rng.uniform(0.5, 1.5, w[k].shape).astype(np.float32)
+    path = os.path.join(tmpdir_mod, "llama3_head.npz")
+    synth.save_npz(path, w)
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    ids = rng.integers(0, args.vocab_size, (8, 12))
+    got, want = m(ids, 0), ref(ids, 0)
+    _close(got, want)
+    pos = 12
+    for _ in range(5):
+        nxt = want[:, -1, :].argmax(-1)[:, None]
+        got, want = m(nxt, pos), ref(nxt, pos)
+        _close(got, want)
+        pos += 1
