@@ -22,15 +22,19 @@
 // and a range of queries.  Wave w works for head g = w % G; the 4/G waves of one head share its
 // 16-query blocks, dealt zig-zag (w, 7-w, 8+w, 15-w for 4 waves) so causal work is balanced.
 // K/V tiles of KT keys are staged through double-buffered LDS (K rows padded to HD+8 floats:
-// conflict-free ds_read_b128).  Tiles / 16-key groups past a block's last query are skipped.
+// conflict-free ds_read_b128).  Tiles / 16-key groups past a block's last query are skipped;
+// only a q-block's diagonal tile runs the masked body (per-group liveness + causal compare),
+// every other tile a branch-free one (C3 attention +3.8 %, bit-identical results).
 #pragma once
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace l3 {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int HD, int QBW, int G, int KT, bool JOINT = false>
+template <int HD, int QBW, int G, int KT>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (G == 1 || G == 2 || G == 4), "shape");
     constexpr int WPH = 4 / G;                // waves per head
@@ -123,101 +127,20 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
         const int cur = tile & 1;
         if (tile + 1 < ntiles) gload(tile + 1);
         const int k0 = tile * KT;
-        if constexpr (JOINT) {
-            // phase 1: S^T for every live q-block of this wave
-            f32x4 sacc[QBW][KG];
-            bool live[QBW][KG];
-            bool act[QBW], diag[QBW];
-#pragma unroll
-            for (int j = 0; j < QBW; ++j) {
-                const int qblock_first = q_lo + qblk[j] * 16;
-                const int qmax_abs = start_pos + min(qblock_first + 15, p.L - 1);
-                act[j] = qblock_first < p.L && k0 <= qmax_abs;        // wave-uniform
-                diag[j] = k0 + KT - 1 > start_pos + qblock_first;     // some key is masked
-#pragma unroll
-                for (int kg = 0; kg < KG; ++kg) {
-                    live[j][kg] = act[j] && (k0 + kg * 16) <= qmax_abs;
-                    sacc[j][kg] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    if (live[j][kg]) {
-#pragma unroll
-                        for (int dg = 0; dg < ND; ++dg) {
-                            const f32x4 kf = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
-#pragma unroll
-                            for (int s = 0; s < 4; ++s)
-                                sacc[j][kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qreg[j][dg][s], sacc[j][kg], 0, 0, 0);
-                        }
-                    }
-                }
-            }
-            // phase 2: online softmax per q-block (mask only on diagonal tiles)
-#pragma unroll
-            for (int j = 0; j < QBW; ++j) {
-                if (!act[j]) continue;
-                const int q_abs = start_pos + q_lo + qblk[j] * 16 + fq;
-                float mt = -INFINITY;
-#pragma unroll
-                for (int kg = 0; kg < KG; ++kg)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        float v = sacc[j][kg][r];
-                        if (diag[j]) {
-                            const int key = k0 + kg * 16 + fk + r;
-                            v = (live[j][kg] && key <= q_abs) ? v : -INFINITY;
-                        } else if (!live[j][kg]) {
-                            v = -INFINITY;
-                        }
-                        sacc[j][kg][r] = v;
-                        mt = fmaxf(mt, v);
-                    }
-                mt = fmaxf(mt, __shfl_xor(mt, 16));
-                mt = fmaxf(mt, __shfl_xor(mt, 32));
-                const float m_new = fmaxf(m_run[j], mt);
-                const float alpha = __builtin_amdgcn_exp2f(m_run[j] - m_new);
-                m_run[j] = m_new;
-                float psum = 0.f;
-#pragma unroll
-                for (int kg = 0; kg < KG; ++kg)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-                        const float pv = __builtin_amdgcn_exp2f(sacc[j][kg][r] - m_new);
-                        sacc[j][kg][r] = pv;
-                        psum += pv;
-                    }
-                l_run[j] = l_run[j] * alpha + psum;
-#pragma unroll
-                for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;
-            }
-            // phase 3: P.V, each V operand read once for all q-blocks
-#pragma unroll
-            for (int kg = 0; kg < KG; ++kg) {
-                bool any = false;
-#pragma unroll
-                for (int j = 0; j < QBW; ++j) any |= live[j][kg];
-                if (!any) continue;
-#pragma unroll
-                for (int dg = 0; dg < ND; ++dg)
-#pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        const float vf = Vs[cur][kg * 16 + fk + s][dg * 16 + fq];
-#pragma unroll
-                        for (int j = 0; j < QBW; ++j)
-                            if (live[j][kg])
-                                o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[j][kg][s], o[j][dg], 0, 0, 0);
-                    }
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < QBW; ++j) {
-                const int qblock_first = q_lo + qblk[j] * 16;
-                if (qblock_first >= p.L) continue;                        // padding block
-                const int qmax_abs = start_pos + min(qblock_first + 15, p.L - 1);
-                if (k0 > qmax_abs) continue;                              // whole tile masked
+        {
+            // one q-block against this K/V tile; MASKED: the diagonal tile (some key of the tile
+            // is past some query of the block: per-16-key-group liveness + causal mask).  The
+            // unmasked body has no wave-uniform branches, so hipcc can interleave the four
+            // key groups' S chains and hoist the V reads
+            auto qblock_tile = [&](const int j, const int qblock_first, const int qmax_abs,
+                                   auto masked_tag) {
+                constexpr bool MASKED = decltype(masked_tag)::value;
                 const int q_abs = start_pos + qblock_first + fq;
                 f32x4 sacc[KG];
                 bool live[KG];
 #pragma unroll
                 for (int kg = 0; kg < KG; ++kg) {
-                    live[kg] = (k0 + kg * 16) <= qmax_abs;                // wave-uniform
+                    live[kg] = !MASKED || (k0 + kg * 16) <= qmax_abs;     // wave-uniform
                     sacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
                     if (live[kg]) {
 #pragma unroll
@@ -229,16 +152,14 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                         }
                     }
                 }
-                // causal mask (diagonal tiles only) + tile max; lane holds keys
-                // k0 + kg*16 + fk + r for query q_abs
-                const bool diag = k0 + KT - 1 > start_pos + qblock_first;  // wave-uniform
+                // causal mask + tile max; lane holds keys k0 + kg*16 + fk + r for query q_abs
                 float mt = -INFINITY;
 #pragma unroll
                 for (int kg = 0; kg < KG; ++kg)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         float v = sacc[kg][r];
-                        if (diag) {
+                        if constexpr (MASKED) {
                             const int key = k0 + kg * 16 + fk + r;
                             v = (live[kg] && key <= q_abs) ? v : -INFINITY;
                         }
@@ -275,6 +196,18 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                             o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);
                         }
                 }
+            };
+#pragma unroll
+            for (int j = 0; j < QBW; ++j) {
+                const int qblock_first = q_lo + qblk[j] * 16;
+                if (qblock_first >= p.L) continue;                        // padding block
+                const int qmax_abs = start_pos + min(qblock_first + 15, p.L - 1);
+                if (k0 > qmax_abs) continue;                              // whole tile masked
+                // every key of the tile <= every query of the block: no mask, all groups live
+                if (k0 + KT - 1 <= start_pos + qblock_first)
+                    qblock_tile(j, qblock_first, qmax_abs, std::integral_constant<bool, false>{});
+                else
+                    qblock_tile(j, qblock_first, qmax_abs, std::integral_constant<bool, true>{});
             }
         }
         if (tile + 1 < ntiles) sstore(cur ^ 1);

@@ -28,18 +28,13 @@ struct Variant {
     std::function<void(const AttnArgs&, hipStream_t)> run;
 };
 
-#define AVARJ(HD, QBW, G, KT)                                                                 \
-    Variant{"joint<" #HD ",q" #QBW ",g" #G ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) { \
-                constexpr int QW = 16 * QBW * (4 / G);                                        \
-                dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
-                hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT, true>), grid, dim3(256), 0, s, a); \
-            }}
 #define AVAR(HD, QBW, G, KT)                                                                  \
     Variant{"attn<" #HD ",q" #QBW ",g" #G ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) { \
                 constexpr int QW = 16 * QBW * (4 / G);                                        \
                 dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, dim3(256), 0, s, a); \
             }}
+
 
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
@@ -103,8 +98,8 @@ static void run(const char* label, int B, int L, int H, int KVH, int HD, std::ve
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
     run("stories15M C3", 256, 256, 6, 6, 48,
-        {AVAR(48, 4, 1, 64), AVARJ(48, 4, 1, 64), AVARJ(48, 2, 1, 64), AVARJ(48, 4, 1, 32)}, rounds, iters);
+        {AVAR(48, 4, 1, 64), AVAR(48, 4, 1, 32), AVAR(48, 2, 1, 64)}, rounds, iters);
     run("Llama-3 shape (C5 slice)", 4, 2048, 32, 8, 128,
-        {AVAR(128, 1, 4, 32), AVARJ(128, 1, 4, 32), AVARJ(128, 2, 4, 32)}, rounds, 3);
+        {AVAR(128, 1, 4, 32), AVAR(128, 2, 4, 32)}, rounds, 3);
     return 0;
 }
