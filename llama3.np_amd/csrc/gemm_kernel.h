@@ -67,8 +67,8 @@ __device__ __forceinline__ int lds_swz(int r) {
 // QKV epilogue (same register-direct fragment map as direct_epilogue): RMSNorm row factor,
 // RoPE on the two (even, odd) pairs of each float4 (llama3.py:41-76), then q (scaled) to the q
 // buffer, k / v appended to the KV cache (llama3.py:184-185).  Branch-free over the q/k/v
-// sections (a V tile rotates by cos = 1, sin = 0, which is exact), and every RoPE table load is
-// issued before the first store: a load's vmcnt wait also waits for all older stores.
+// sections (a V tile rotates by cos = 1, sin = 0, which is exact), and the RoPE table loads of
+// each row-half are issued before its stores: a load's vmcnt wait also waits for all older stores.
 template <int TM, int TN>
 __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&acc)[TM][TN],
                                              const float (&rs)[TM], int mrow0, int ncol0,
@@ -92,33 +92,40 @@ __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&ac
         head[j] = cc / p.HD;
         d[j] = cc - head[j] * p.HD;
     }
-    float2 cs[TM][TN], sn[TM][TN];
+    // two row-halves: each issues its RoPE loads (TM/2 x TN pairs) before its stores, so a
+    // wave waits twice rather than once per float4, and the 4-block/CU register budget holds
+    constexpr int TH = TM > 1 ? TM / 2 : 1;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i0 = 0; i0 < TM; i0 += TH) {
+        float2 cs[TH][TN], sn[TH][TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int t = pos[i] * hd2 + (d[j] >> 1);
-            cs[i][j] = *reinterpret_cast<const float2*>(p.rope_cos + t);
-            sn[i][j] = *reinterpret_cast<const float2*>(p.rope_sin + t);
-        }
+        for (int ii = 0; ii < TH; ++ii)
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int row = mrow0 + i * 16 + frow;
+            for (int j = 0; j < TN; ++j) {
+                const int t = pos[i0 + ii] * hd2 + (d[j] >> 1);
+                cs[ii][j] = *reinterpret_cast<const float2*>(p.rope_cos + t);
+                sn[ii][j] = *reinterpret_cast<const float2*>(p.rope_sin + t);
+            }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = ncol0 + j * 16 + fq4;
-            if (row >= p.M || col >= p.N) continue;
-            const bool rot = sec[j] < 2;
-            const float2 c = rot ? cs[i][j] : float2{1.f, 1.f};
-            const float2 s = rot ? sn[i][j] : float2{0.f, 0.f};
-            const f32x4 v = acc[i][j] * (sec[j] == 0 ? rs[i] * p.q_scale : rs[i]);
-            const f32x4 r = {v.x * c.x - v.y * s.x, v.x * s.x + v.y * c.x,
-                             v.z * c.y - v.w * s.y, v.z * s.y + v.w * c.y};
-            float* base = sec[j] == 0 ? p.q_out : (sec[j] == 1 ? p.cache_k : p.cache_v);
-            const int64_t off = sec[j] == 0
-                                    ? (int64_t)row * qdim + col
-                                    : (((int64_t)bidx[i] * p.KVH + head[j]) * p.Smax + pos[i]) * p.HD + d[j];
-            *reinterpret_cast<f32x4*>(base + off) = r;
+        for (int ii = 0; ii < TH; ++ii) {
+            const int i = i0 + ii;
+            const int row = mrow0 + i * 16 + frow;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = ncol0 + j * 16 + fq4;
+                if (row >= p.M || col >= p.N) continue;
+                const bool rot = sec[j] < 2;
+                const float2 c = rot ? cs[ii][j] : float2{1.f, 1.f};
+                const float2 s = rot ? sn[ii][j] : float2{0.f, 0.f};
+                const f32x4 v = acc[i][j] * (sec[j] == 0 ? rs[i] * p.q_scale : rs[i]);
+                const f32x4 r = {v.x * c.x - v.y * s.x, v.x * s.x + v.y * c.x,
+                                 v.z * c.y - v.w * s.y, v.z * s.y + v.w * c.y};
+                float* base = sec[j] == 0 ? p.q_out : (sec[j] == 1 ? p.cache_k : p.cache_v);
+                const int64_t off = sec[j] == 0
+                                        ? (int64_t)row * qdim + col
+                                        : (((int64_t)bidx[i] * p.KVH + head[j]) * p.Smax + pos[i]) * p.HD + d[j];
+                *reinterpret_cast<f32x4*>(base + off) = r;
+            }
         }
     }
 }
