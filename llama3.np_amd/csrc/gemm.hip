@@ -20,7 +20,8 @@ template <int EPI, int MR, int LPU>
 static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
     const int units = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? a.N / 2 : a.N;
     const int per_block = 4 * (64 / LPU);
-    const dim3 grid((unsigned)((units + per_block - 1) / per_block)), block(256);
+    const dim3 grid((unsigned)((units + per_block - 1) / per_block), (unsigned)((a.M + MR - 1) / MR)),
+        block(256);
     hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU>), grid, block, (size_t)MR * a.K * 4, s, a);
     return hipGetLastError();
 }
@@ -47,9 +48,13 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.K % 32 != 0 || a.K <= 0) return hipErrorInvalidValue;  // whole 32-deep k-tiles
     if (epi == EPI_SWIGLU && a.N % 32 != 0) return hipErrorInvalidValue;
     if (a.N % 4 != 0 || a.ldc % 4 != 0 || a.lda % 4 != 0) return hipErrorInvalidValue;  // 16-B rows
-    // M <= 8 (decode, short prompts): weight-streaming GEMV with the same epilogues
+    // Short M (decode, batched decode, short prompts): weight-streaming GEMV with the same
+    // epilogues, 8-row blocks beyond M = 8 re-reading W through L2 — for the layer weights up
+    // to M = 256 (a 128-row MFMA tile there is one k-loop of memory round trips on a handful of
+    // blocks); the 37 MB lm_head keeps the MFMA tiles past M = 8
     const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
-    if (a.M <= 8 && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS (QKV: N even)
+    const bool short_m = a.M <= 8 || (a.M <= 256 && (int64_t)a.N * a.K <= (int64_t)4 << 20);
+    if (short_m && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS (QKV: N even)
         switch (epi) {
             case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);
             case EPI_QKV: return launch_gemv<EPI_QKV>(a, s);

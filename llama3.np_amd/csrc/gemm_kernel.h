@@ -383,8 +383,8 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 #undef L3_STAMP
 
 // ---------------------------------------------------------------------------------------
-// Skinny GEMM for M <= 8 rows (greedy decode, short prompts): weight-streaming, HBM / latency
-// bound, so no MFMA.  A unit is one W row (EPI_STORE / EPI_RESID), a RoPE pair (EPI_QKV: rows
+// Skinny GEMM for short M (greedy decode, short prompts): weight-streaming, HBM / latency
+// bound, so no MFMA; MR rows per block, grid.y row blocks beyond MR.  A unit is one W row (EPI_STORE / EPI_RESID), a RoPE pair (EPI_QKV: rows
 // 2u, 2u + 1) or a gate/up pair (EPI_SWIGLU: fused rows 32(u/16) + u%16 and + 16).  LPU lanes
 // share a unit and split its K: lane j streams float4 k4 = j + LPU t, with a whole chunk of CH
 // loads per row in flight before the first FMA (one memory round trip per chunk, not one per
@@ -425,10 +425,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                 w[r][t] = k4 < K4 ? W4[(int64_t)wrow[r] * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
         }
     };
+    // row block: rows [m0, m0 + Mb) of A (grid.y row blocks of MR rows re-read W through L2)
+    const int m0 = blockIdx.y * MR, Mb = min(MR, p.M - m0);
     load_chunk(0);  // in flight while the input rows are staged
-    for (int f = tid; f < p.M * K4; f += 256) {
+    for (int f = tid; f < Mb * K4; f += 256) {
         const int m = f / K4, k4 = f - m * K4;
-        reinterpret_cast<f32x4*>(xs)[f] = reinterpret_cast<const f32x4*>(p.A + (int64_t)m * p.lda)[k4];
+        reinterpret_cast<f32x4*>(xs)[f] = reinterpret_cast<const f32x4*>(p.A + (int64_t)(m0 + m) * p.lda)[k4];
     }
     __syncthreads();
 
@@ -448,7 +450,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             if (k4 >= K4) break;
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
-                if (m >= p.M) break;
+                if (m >= Mb) break;
                 const f32x4 x = reinterpret_cast<const f32x4*>(xs + m * p.K)[k4];
                 ss[m] += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
 #pragma unroll
@@ -467,14 +469,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
         }
     if (j != 0 || !valid) return;
 #pragma unroll
-    for (int m = 0; m < MR; ++m) {
-        if (m >= p.M) break;
-        const float sc = p.norm ? 1.0f / sqrtf(ss[m] / (float)p.K + p.eps) : 1.0f;
+    for (int mi = 0; mi < MR; ++mi) {
+        if (mi >= Mb) break;
+        const int m = m0 + mi;  // global row
+        const float sc = p.norm ? 1.0f / sqrtf(ss[mi] / (float)p.K + p.eps) : 1.0f;
         if constexpr (EPI == EPI_QKV) {
             // columns 2u, 2u + 1: one RoPE pair (llama3.py:41-76), then q / KV-cache append
             const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
             const int col = 2 * unit;
-            float v0 = acc[0][m] * sc, v1 = acc[ROWS - 1][m] * sc;
+            float v0 = acc[0][mi] * sc, v1 = acc[ROWS - 1][mi] * sc;
             const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
             const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
             const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
@@ -492,9 +495,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             *dst = is_q ? float2{v0 * p.q_scale, v1 * p.q_scale} : float2{v0, v1};
         } else {
             float* dst = p.C + (int64_t)m * p.ldc + unit;
-            if constexpr (EPI == EPI_SWIGLU) *dst = silu_f(acc[0][m] * sc) * (acc[ROWS - 1][m] * sc);
-            else if constexpr (EPI == EPI_RESID) *dst += acc[0][m];
-            else *dst = acc[0][m] * sc;
+            if constexpr (EPI == EPI_SWIGLU) *dst = silu_f(acc[0][mi] * sc) * (acc[ROWS - 1][mi] * sc);
+            else if constexpr (EPI == EPI_RESID) *dst += acc[0][mi];
+            else *dst = acc[0][mi] * sc;
         }
     }
 }

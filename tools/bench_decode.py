@@ -24,6 +24,22 @@ def main():
     eager = "--eager" in sys.argv  # profiling: every step eager, no device-loop leg
     if eager:
         os.environ["L3_DECODE_GRAPH"] = "0"
+    if "--eager-batch" in sys.argv:  # profiling: 40 eager steps of one B-row batch
+        os.environ["L3_DECODE_GRAPH"] = "0"
+        B = int(sys.argv[sys.argv.index("--eager-batch") + 1])
+        gb = np.load(os.path.join(REPO, "tests", "golden", "stories15m_default.npz"))
+        argsb = synth.stories15m(B)
+        wb = synth.make_weights(argsb, synth.STORIES15M_HIDDEN, seed=int(gb["seed"]))
+        with tempfile.TemporaryDirectory() as d:
+            p = os.path.join(d, "w.npz")
+            synth.save_npz(p, wb)
+            mb = llama3.Llama(p, argsb)
+        pr = np.random.default_rng(B).integers(3, argsb.vocab_size, (B, 5))
+        t0 = time.perf_counter()
+        n = sum(1 for _ in mb.generate(pr, 45))
+        t = time.perf_counter() - t0
+        print(json.dumps({"workload": f"stories15M greedy decode B={B} (eager)", "ms_per_step": round(t / n * 1e3, 3)}))
+        return
     g = np.load(os.path.join(REPO, "tests", "golden", "stories15m_default.npz"))
     args = synth.stories15m(1)
     w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=int(g["seed"]), preset="default")
@@ -53,13 +69,30 @@ def main():
         dev.append(time.perf_counter() - t0)
     td = float(np.median(dev))
     exact_all = all_ids[0].tolist() == g["dream_ids"][0].tolist()
+    # batched device-side loop: B synthetic 5-token prompts, 145 steps
+    batched = {}
+    for B in (8, 64, 256):
+        argsb = synth.stories15m(B)
+        with tempfile.TemporaryDirectory() as d:
+            p = os.path.join(d, "w.npz")
+            synth.save_npz(p, w)
+            mb = llama3.Llama(p, argsb)
+        pr = np.random.default_rng(B).integers(3, argsb.vocab_size, (B, prompt.shape[1]))
+        mb.generate_all(pr, 20)  # warm-up + graph capture for this B
+        t0 = time.perf_counter()
+        out = mb.generate_all(pr, int(g["dream_max_new"]))
+        tb = time.perf_counter() - t0
+        batched[str(B)] = {"generated_tokens_per_s": round(out.size / tb, 1),
+                           "ms_per_step": round(tb / out.shape[1] * 1e3, 3)}
+        del mb
     print(json.dumps({"workload": "stories15M greedy decode B=1, 'I have a dream', 145 steps",
                       "tokens_per_s_reference_count": round(count / t, 1),
                       "generated_tokens_per_s": round(len(ids) / t, 1),
                       "ms_per_step": round(t / len(ids) * 1e3, 3), "ids_exact_vs_reference": exact,
                       "device_loop_generated_tokens_per_s": round(len(ids) / td, 1),
                       "device_loop_ms_per_step": round(td / len(ids) * 1e3, 3),
-                      "device_loop_ids_exact": exact_all}))
+                      "device_loop_ids_exact": exact_all,
+                      "batched_device_loop": batched}))
 
 
 if __name__ == "__main__":
