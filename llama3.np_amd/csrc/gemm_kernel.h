@@ -428,9 +428,20 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     // row block: rows [m0, m0 + Mb) of A (grid.y row blocks of MR rows re-read W through L2)
     const int m0 = blockIdx.y * MR, Mb = min(MR, p.M - m0);
     load_chunk(0);  // in flight while the input rows are staged
-    for (int f = tid; f < Mb * K4; f += 256) {
-        const int m = f / K4, k4 = f - m * K4;
-        reinterpret_cast<f32x4*>(xs)[f] = reinterpret_cast<const f32x4*>(p.A + (int64_t)(m0 + m) * p.lda)[k4];
+    // stage the row block (rows past Mb zero: branch-free FMA loop), SU loads in flight per
+    // thread before the first LDS store (a serial load -> store walk costs a round trip each)
+    constexpr int SU = 8;
+    for (int f0 = tid; f0 < MR * K4; f0 += 256 * SU) {
+        f32x4 v[SU];
+#pragma unroll
+        for (int u = 0; u < SU; ++u) {
+            const int f = f0 + 256 * u, m = f / K4, k4 = f - m * K4;
+            v[u] = (f < MR * K4 && m < Mb) ? reinterpret_cast<const f32x4*>(p.A + (int64_t)(m0 + m) * p.lda)[k4]
+                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int u = 0; u < SU; ++u)
+            if (f0 + 256 * u < MR * K4) reinterpret_cast<f32x4*>(xs)[f0 + 256 * u] = v[u];
     }
     __syncthreads();
 
@@ -446,16 +457,19 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
         if (t0) load_chunk(t0);
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
-            const int k4 = j + LPU * (t0 + t);
-            if (k4 >= K4) break;
+            if (t0 + t >= nt) break;  // wave-uniform
+            // lanes past K read a clamped (finite) x against their zero W and count no norm
+            const int k4 = j + LPU * (t0 + t), kk = min(k4, K4 - 1);
+            const float in = k4 < K4 ? 1.f : 0.f;
+            f32x4 x[MR];
+#pragma unroll
+            for (int m = 0; m < MR; ++m) x[m] = reinterpret_cast<const f32x4*>(xs + m * p.K)[kk];
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
-                if (m >= Mb) break;
-                const f32x4 x = reinterpret_cast<const f32x4*>(xs + m * p.K)[k4];
-                ss[m] += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+                ss[m] += in * (x[m].x * x[m].x + x[m].y * x[m].y + x[m].z * x[m].z + x[m].w * x[m].w);
 #pragma unroll
                 for (int r = 0; r < ROWS; ++r)
-                    acc[r][m] += w[r][t].x * x.x + w[r][t].y * x.y + w[r][t].z * x.z + w[r][t].w * x.w;
+                    acc[r][m] += w[r][t].x * x[m].x + w[r][t].y * x[m].y + w[r][t].z * x[m].z + w[r][t].w * x[m].w;
             }
         }
     }
