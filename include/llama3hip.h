@@ -63,7 +63,9 @@ enum l3_weight_kind {
     L3_W_LM_HEAD = 11    /* lm_head.weight                       [VS, D]        */
 };
 
-/* Kernel ids for l3_kernel_stats (per-kind HIP-event timing). */
+/* Kernel ids for l3_kernel_stats (per-kind HIP-event timing).  L3_K_EMBED counts nothing
+ * since layer 0 gathers its input rows from the embedding table (llama3.py:287 fused into
+ * its QKV and O-proj launches); the id is kept so the numbering stays stable. */
 enum l3_kernel_id {
     L3_K_EMBED = 0, L3_K_QKV = 1, L3_K_ATTN = 2, L3_K_OPROJ = 3, L3_K_GATEUP = 4,
     L3_K_DOWN = 5, L3_K_LMHEAD = 6, L3_K_ARGMAX = 7, L3_K_GATHER = 8, L3_K_COUNT = 9

@@ -165,7 +165,7 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
                 float* dst = p.C + (int64_t)row * p.ldc + col;
                 if constexpr (EPI == EPI_RESID) {
                     if constexpr (RES_PREFETCH) v += res[i * TN + j];
-                    else v += *reinterpret_cast<const f32x4*>(dst);
+                    else v += *reinterpret_cast<const f32x4*>(res_at(p, row, col));
                 } else {
                     v *= sc;
                 }
@@ -220,15 +220,23 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     // ---- k-tile fill, GLDS: one wave-instruction writes 1 KB = RP image rows (lane i at byte
     // 16 i); the swizzle moves to the source address.  Pieces go round-robin over the waves;
     // rows past M / N are clamped (their outputs are never stored).
+    // A-row source addresses are fixed for the tile: resolved once (a gathered embedding row
+    // costs one index load per lane here, never inside the k-loop beside the DMA)
+    constexpr int A_PIECES = (BM / RP + 3) / 4;
+    const float* a_src[A_PIECES];
+#pragma unroll
+    for (int it = 0; it < A_PIECES; ++it) {
+        const int piece = wid + 4 * it, r = piece * RP + lane / Q;
+        a_src[it] = a_row(p, min(m0 + r, p.M - 1)) + 4 * ((lane % Q) ^ lds_swz<BK>(r));
+    }
     auto glds_tile = [&](int buf, int k0) {
         const int rl = lane / Q, pq = lane % Q;
 #pragma unroll
-        for (int it = 0; it < (BM / RP + 3) / 4; ++it) {
-            const int piece = wid + 4 * it, r = piece * RP + rl;
+        for (int it = 0; it < A_PIECES; ++it) {
+            const int piece = wid + 4 * it;
             if ((BM / RP) % 4 == 0 || piece < BM / RP) {
-                const int gm = min(m0 + r, p.M - 1), q = pq ^ lds_swz<BK>(r);
                 __builtin_amdgcn_global_load_lds(
-                    (const __attribute__((address_space(1))) void*)(p.A + (int64_t)gm * p.lda + k0 + 4 * q),
+                    (const __attribute__((address_space(1))) void*)(a_src[it] + k0),
                     (__attribute__((address_space(3))) void*)&As[buf][piece * RP][0], 16, 0, 0);
             }
         }
@@ -251,7 +259,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             const int f = tid + 256 * i, row = f / Q, c = (f % Q) * 4, gm = m0 + row;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
             if ((A_F4 % 256 == 0 || f < A_F4) && gm < p.M)
-                v = *reinterpret_cast<const f32x4*>(p.A + (int64_t)gm * p.lda + k0 + c);
+                v = *reinterpret_cast<const f32x4*>(a_row(p, gm) + k0 + c);
             ra[i] = v;
         }
 #pragma unroll
@@ -348,7 +356,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             for (int j = 0; j < TN; ++j) {
                 const int row = m0 + arow0 + i * 16 + frow, col = n0 + brow0 + j * 16 + fk;
                 res[i * TN + j] = (row < p.M && col < p.N)
-                                      ? *reinterpret_cast<const f32x4*>(p.C + (int64_t)row * p.ldc + col)
+                                      ? *reinterpret_cast<const f32x4*>(res_at(p, row, col))
                                       : f32x4{0.f, 0.f, 0.f, 0.f};
             }
     }
@@ -436,7 +444,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
 #pragma unroll
         for (int u = 0; u < SU; ++u) {
             const int f = f0 + 256 * u, m = f / K4, k4 = f - m * K4;
-            v[u] = (f < MR * K4 && m < Mb) ? reinterpret_cast<const f32x4*>(p.A + (int64_t)(m0 + m) * p.lda)[k4]
+            v[u] = (f < MR * K4 && m < Mb) ? reinterpret_cast<const f32x4*>(a_row(p, m0 + m))[k4]
                                            : f32x4{0.f, 0.f, 0.f, 0.f};
         }
 #pragma unroll
@@ -510,7 +518,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
         } else {
             float* dst = p.C + (int64_t)m * p.ldc + unit;
             if constexpr (EPI == EPI_SWIGLU) *dst = silu_f(acc[0][mi] * sc) * (acc[ROWS - 1][mi] * sc);
-            else if constexpr (EPI == EPI_RESID) *dst += acc[0][mi];
+            else if constexpr (EPI == EPI_RESID) *dst = *res_at(p, m, unit) + acc[0][mi];
             else *dst = acc[0][mi] * sc;
         }
     }

@@ -29,7 +29,21 @@ struct GemmArgs {
     const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
     unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 10 per block
+    // Embedding fused into layer 0 (llama3.py:287): when set, A row r is A + a_rows[r] * lda
+    // (the token's embedding row) and EPI_RESID adds res_src[res_rows[r] * ldc + col] instead
+    // of reading C, so the residual stream h is first written by layer 0's O-proj
+    const int32_t* a_rows;
+    const float* res_src; const int32_t* res_rows;
 };
+
+// row r of A (identity, or the gathered embedding row)
+__device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
+    return p.A + (p.a_rows ? (int64_t)p.a_rows[r] : r) * p.lda;
+}
+// residual operand of EPI_RESID at (row, col): C itself, or the gathered embedding row
+__device__ __forceinline__ const float* res_at(const GemmArgs& p, int64_t row, int col) {
+    return p.res_src ? p.res_src + (int64_t)p.res_rows[row] * p.ldc + col : p.C + row * p.ldc + col;
+}
 
 struct AttnArgs {
     const float* q;       // [B*L, H*HD], pre-scaled by log2(e)/sqrt(HD)
@@ -48,8 +62,6 @@ __device__ __forceinline__ int start_of(const Args& p) {
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
-hipError_t launch_embed(const int32_t* ids, const float* emb, float* h, int64_t T, int D,
-                        hipStream_t s);
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
                          int* pos_dev = nullptr);
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s);

@@ -1,4 +1,4 @@
-// Bandwidth-bound helper kernels for gfx950: embedding gather, greedy argmax, and the
+// Bandwidth-bound helper kernels for gfx950: greedy argmax and the
 // op-level kernels behind the reference's module functions.  Loads are 16 B per lane where the layout allows (rows are multiples of 4 floats), one wavefront-wide
 // reduction per row for the row ops.
 #include "kernels.h"
@@ -16,18 +16,6 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
     return v;
-}
-
-// h[t, :] = emb[ids[t], :]   (llama3.py:287).  ids validated on the host.
-__global__ void embed_kernel(const int32_t* __restrict__ ids, const float* __restrict__ emb,
-                             float* __restrict__ h, int64_t T, int D4) {
-    const int64_t total = T * D4;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = i / D4;
-        const int c = (int)(i - t * D4);
-        reinterpret_cast<f32x4*>(h)[i] = reinterpret_cast<const f32x4*>(emb)[(int64_t)ids[t] * D4 + c];
-    }
 }
 
 // argmax over each row with np.argmax's first-index tie-break (llama3.py:320); a NaN wins
@@ -161,14 +149,6 @@ static inline unsigned grid_for(int64_t n, int block) {
     int64_t g = (n + block - 1) / block;
     if (g > 4096) g = 4096;
     return (unsigned)(g < 1 ? 1 : g);
-}
-
-hipError_t launch_embed(const int32_t* ids, const float* emb, float* h, int64_t T, int D,
-                        hipStream_t s) {
-    if (D % 4) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(embed_kernel, dim3(grid_for(T * (D / 4), 256)), dim3(256), 0, s, ids, emb, h,
-                       T, D / 4);
-    return hipGetLastError();
 }
 
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,

@@ -446,7 +446,11 @@ static int check_call(l3_ctx* c, int B, int L, int start_pos) {
 }
 
 // one transformer block on the residual stream c->h [B*L, D] (llama3.py:239-261)
-static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* pos_dev = nullptr) {
+// emb_ids: layer 0 of a model forward reads its input rows straight from the embedding table
+// (llama3.py:287 fused into the QKV GEMM's A gather and the O-proj's residual), so no embed
+// kernel runs and h is first written by that O-proj
+static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* pos_dev = nullptr,
+                     const int32_t* emb_ids = nullptr) {
     Layer& Ly = c->layers[li];
     const int64_t T = (int64_t)B * L;
     const int D = c->d.dim, FD = c->d.hidden_dim;
@@ -461,6 +465,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     g.Smax = c->d.max_seq_len;
     g.pos_dev = pos_dev;
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
+    if (emb_ids) { g.A = c->emb; g.a_rows = emb_ids; }
     if (timed(c, L3_K_QKV, [&] { return launch_gemm(EPI_QKV, g, c->stream); })) return 1;
     // causal attention over the cache
     AttnArgs a{};
@@ -472,6 +477,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     GemmArgs o{};
     o.A = c->attn; o.lda = c->qdim; o.W = Ly.wo; o.C = c->h; o.ldc = D;
     o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
+    if (emb_ids) { o.res_src = c->emb; o.res_rows = emb_ids; }  // h = emb[ids] + attn . Wo^T
     if (timed(c, L3_K_OPROJ, [&] { return launch_gemm(EPI_RESID, o, c->stream); })) return 1;
     // rmsnorm -> gate|up -> SwiGLU
     GemmArgs gu{};
@@ -489,12 +495,9 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
 
 static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
                        float* logits_dev, const int* pos_dev = nullptr) {
-    const int64_t T = (int64_t)B * L;
     const int D = c->d.dim;
-    if (timed(c, L3_K_EMBED, [&] { return launch_embed(ids_dev, c->emb, c->h, T, D, c->stream); }))
-        return 1;
     for (int li = 0; li < (int)c->layers.size(); ++li)
-        if (run_layer(c, li, B, L, start_pos, pos_dev)) return 1;
+        if (run_layer(c, li, B, L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr)) return 1;
     // final RMSNorm + lm_head on the last position of each sequence (llama3.py:304-307)
     GemmArgs lm{};
     lm.A = c->h + (int64_t)(L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
