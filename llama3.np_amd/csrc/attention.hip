@@ -43,16 +43,20 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (a.L == 1 && a.Smax <= 8192) {  // decode: one query per (b, h)
         switch (a.HD) {
             case 16: return launch_decode<16>(a, s);
+            case 32: return launch_decode<32>(a, s);
             case 48: return launch_decode<48>(a, s);
             case 64: return launch_decode<64>(a, s);
+            case 96: return launch_decode<96>(a, s);
             case 128: return launch_decode<128>(a, s);
             default: return hipErrorInvalidValue;
         }
     }
     switch (a.HD) {
         case 16: return launch_hd<16, 64, 4>(a, s);
+        case 32: return launch_hd<32, 64, 4>(a, s);
         case 48: return launch_hd<48, 64, 4>(a, s);
         case 64: return launch_hd<64, 64, 4>(a, s);
+        case 96: return launch_hd<96, 32, 1>(a, s);   // KT 32: 52 KB LDS -> 2 workgroups per CU
         case 128: return launch_hd<128, 32, 1>(a, s);  // KT 32: 72 KB LDS -> 2 workgroups per CU
         default: return hipErrorInvalidValue;
     }

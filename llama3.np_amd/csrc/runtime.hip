@@ -218,8 +218,10 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     if (d.n_layers > 0 && (HD % 16 || d.dim % 32 || d.hidden_dim % 32))
         return fail("l3_create: need head_dim %% 16 == 0, dim %% 32 == 0, hidden %% 32 == 0 "
                     "(got HD %d, D %d, FD %d)", HD, d.dim, d.hidden_dim);
-    if (d.n_layers > 0 && !(HD == 16 || HD == 48 || HD == 64 || HD == 128))
-        return fail("l3_create: head_dim %d has no attention instantiation", HD);
+    if (d.n_layers > 0 && !(HD == 16 || HD == 32 || HD == 48 || HD == 64 || HD == 96 || HD == 128))
+        return fail("l3_create: head_dim %d has no attention instantiation (16, 32, 48, 64, 96, 128)", HD);
+    if (d.n_layers > 0 && d.vocab_size % 4)  // logits rows leave the lm_head GEMM as 16-byte stores
+        return fail("l3_create: vocab_size %d must be a multiple of 4", d.vocab_size);
     l3_ctx* c = new l3_ctx();
     c->device = device;
     c->d = d;

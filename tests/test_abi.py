@@ -58,3 +58,18 @@ def test_dims_struct_layout():
 
 def test_library_path_is_in_tree():
     assert os.path.dirname(l3hip.LIB_PATH).endswith(os.path.join("llama3.np_amd", "csrc"))
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(dim=320, n_heads=4, n_kv_heads=4), "head_dim 80 has no attention instantiation"),
+    (dict(dim=304, n_heads=1, n_kv_heads=1), "dim % 32 == 0"),
+    (dict(vocab_size=32001), "vocab_size 32001 must be a multiple of 4"),
+    (dict(n_heads=6, n_kv_heads=4), "n_heads % n_kv_heads"),
+])
+def test_create_rejects_unsupported_shapes_before_touching_a_device(kw, msg):
+    """Shape limits of the kernels are checked up front with a message (no GPU needed)."""
+    d = dict(dim=288, n_layers=6, n_heads=6, n_kv_heads=6, vocab_size=32000, hidden_dim=768,
+             max_seq_len=256, max_batch_size=1, norm_eps=1e-6)
+    d.update(kw)
+    with pytest.raises(RuntimeError, match=re.escape(msg)):
+        l3hip.Context(l3hip.Dims(**d), 0)

@@ -295,20 +295,22 @@ def test_generate_all_batched_matches_oracle(tmpdir_mod):
             np.testing.assert_array_equal(got, orc.greedy_ids(ref, prompt, n))
 
 
-def test_llama3_head_dim_gqa_decode_with_norm_weights(tmpdir_mod):
-    """Llama-3 head geometry (HD = 128, n_rep = 4) with non-unit RMSNorm weights (exercises the
-    fold into W): prefill at B = 8, L = 40, then five L = 1 decode steps at B = 8
-    (decode attention, GEMV epilogues) fed the oracle's own ids, logits compared every step."""
+@pytest.mark.parametrize("dim,heads,kv_heads", [(512, 4, 1), (128, 4, 2), (192, 2, 1)])
+def test_head_dims_gqa_decode_with_norm_weights(tmpdir_mod, dim, heads, kv_heads):
+    """Head geometries beyond stories15M's 48 — HD = 128 (Llama-3, n_rep = 4), 32 and 96 — with
+    non-unit RMSNorm weights (exercises the fold into W): prefill at B = 8, L = 40, then five
+    L = 1 decode steps at B = 8 (decode attention, GEMV epilogues) fed the oracle's own ids,
+    logits compared every step."""
     from config import ModelArgs
 
-    args = ModelArgs(dim=512, n_layers=2, n_heads=4, n_kv_heads=1, vocab_size=1000,
+    args = ModelArgs(dim=dim, n_layers=2, n_heads=heads, n_kv_heads=kv_heads, vocab_size=1000,
                      max_seq_len=96, max_batch_size=8)
-    w = synth.make_weights(args, 1024, seed=11, preset="default")
+    w = synth.make_weights(args, 2 * dim, seed=11, preset="default")
     rng = np.random.default_rng(12)
     for k in list(w):
         if k.endswith("norm.weight") or k.endswith("layernorm.weight"):
             w[k] = rng.uniform(0.5, 1.5, w[k].shape).astype(np.float32)
-    path = os.path.join(tmpdir_mod, "llama3_head.npz")
+    path = os.path.join(tmpdir_mod, f"head_{dim}_{heads}_{kv_heads}.npz")
     synth.save_npz(path, w)
     m = llama3.Llama(path, args)
     ref = orc.OracleModel(w, args)
