@@ -36,6 +36,8 @@ for s in "$@"; do
     c5small) step c5small 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
     rccl1) step rccl1 180 python tools/rccl_selftest.py --world 1 ;;
+    torchrun1) step torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    cabi) step cabi 300 python -u -m pytest tests/test_c_abi_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
