@@ -359,3 +359,24 @@ def test_cli_end_to_end_on_synthetic_vocab(tmpdir_mod, capsys):
             break
         text += tok.decode([t])
     assert out.startswith("\nI have a dream" + text + "\n\nToken count:"), out[:300]
+
+
+def test_cache_edges_full_context_single_token_prompt(tmpdir_mod):
+    """Edges of the KV cache vs the live oracle on the GQA tiny model at B = max_batch_size:
+    a one-token prompt (L = 1 at position 0: the decode attention with one key), a chunk that
+    ends one short of max_seq_len, then decode steps up to the last slot (max_seq_len - 1)."""
+    args = synth.tiny(4)
+    w, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, 9, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(31)
+    B, M = args.max_batch_size, args.max_seq_len
+    one = rng.integers(0, args.vocab_size, (B, 1))
+    _close(m(one, 0), ref(one, 0))
+    chunk = rng.integers(0, args.vocab_size, (B, M - 4))
+    got, want = m(chunk, 1), ref(chunk, 1)  # positions 1 .. M - 4
+    _close(got, want)
+    for pos in range(M - 3, M):  # the last three slots, one token each
+        nxt = want[:, -1, :].argmax(-1)[:, None]
+        got, want = m(nxt, pos), ref(nxt, pos)
+        _close(got, want)
