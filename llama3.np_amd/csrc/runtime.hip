@@ -16,6 +16,7 @@
 //              logits [B, VS], ids [T], argmax [B]   (grown on demand, T = B*L)
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <cmath>
 #include <cstdarg>
@@ -498,16 +499,27 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
 static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
                        float* logits_dev, const int* pos_dev = nullptr) {
     const int D = c->d.dim;
-    for (int li = 0; li < (int)c->layers.size(); ++li)
-        if (run_layer(c, li, B, L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr)) return 1;
+    // roctx ranges (host-side launch spans; `rocprofv3 --marker-trace`) per block and lm_head
+    static const char* names[] = {"l3.layer0", "l3.layer1", "l3.layer2", "l3.layer3", "l3.layer4",
+                                  "l3.layer5", "l3.layer6", "l3.layer7", "l3.layerN"};
+    roctxRangePushA("l3.forward");
+    for (int li = 0; li < (int)c->layers.size(); ++li) {
+        roctxRangePushA(names[li < 8 ? li : 8]);
+        const int rc = run_layer(c, li, B, L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr);
+        roctxRangePop();
+        if (rc) { roctxRangePop(); return 1; }
+    }
     // final RMSNorm + lm_head on the last position of each sequence (llama3.py:304-307)
+    roctxRangePushA("l3.lm_head");
     GemmArgs lm{};
     lm.A = c->h + (int64_t)(L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
     lm.C = logits_dev; lm.ldc = c->d.vocab_size;
     lm.M = B; lm.N = c->d.vocab_size; lm.K = D; lm.norm = true;  // final norm folded
     lm.eps = c->d.norm_eps;
-    if (timed(c, L3_K_LMHEAD, [&] { return launch_gemm(EPI_STORE, lm, c->stream); })) return 1;
-    return 0;
+    const int rc = timed(c, L3_K_LMHEAD, [&] { return launch_gemm(EPI_STORE, lm, c->stream); });
+    roctxRangePop();
+    roctxRangePop();
+    return rc;
 }
 
 static int upload_ids(l3_ctx* c, const int64_t* ids_host, int64_t T) {
