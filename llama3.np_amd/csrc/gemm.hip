@@ -9,11 +9,11 @@ namespace l3 {
 // Product kernels: k-tiles filled by global_load_lds (GLDS) and the register-direct epilogue
 // (DIRECT): RMSNorm weights are folded into W at l3_finalize, the row factor comes from the A
 // fragments, the tile leaves from registers.
-template <int EPI, int WM, int WN, int TM, int TN, int WPE, int BK>
+template <int EPI, int WM, int WN, int TM, int TN, int WPE, int BK, int NS = 2>
 static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>),
+    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, NS>),
                        dim3((unsigned)tiles), dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -90,9 +90,11 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
                 return a.K <= 512 ? launch<EPI_RESID, 2, 2, 2, 3, 3, 32>(a, s)   // 64 x 96
                                   : launch<EPI_RESID, 2, 2, 4, 3, 2, 32>(a, s);  // 128 x 96
             return launch<EPI_RESID, 2, 2, 4, 4, 2, 32>(a, s);                   // 128 x 128
-        case EPI_STORE:   // lm_head, op-level linear
-            if (small_m) return launch<EPI_STORE, 1, 4, 1, 2, 2, 32>(a, s);
-            return launch<EPI_STORE, 2, 2, 4, 4, 3, 16>(a, s);
+        case EPI_STORE:   // lm_head (the 37 MB W streams from HBM past few blocks: deep
+                          // LDS rings, B = 64 lm_head 30.3 -> 18.4 us), op-level linear
+            if (a.M <= 32) return launch<EPI_STORE, 2, 2, 1, 4, 2, 16, 6>(a, s);
+            if (a.M <= 64) return launch<EPI_STORE, 2, 2, 2, 4, 2, 16, 6>(a, s);
+            return launch<EPI_STORE, 2, 2, 4, 4, 2, 16, 4>(a, s);
         default:
             return hipErrorInvalidValue;
     }

@@ -193,21 +193,29 @@ __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
 
 // ---------------------------------------------------------------------------------------
 // Tiled kernel: 256 threads = 4 waves as WM x WN, wave tile (TM x 16) x (TN x 16).
+// counted wait for this wave's vector-memory ops (loads, stores and LDS-DMA alike, in order)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false,
-          int BK = 32, bool GLDS = true>
+          int BK = 32, bool GLDS = true, int NS = 2>
 __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
     constexpr int BM = WM * TM * 16;
     constexpr int BN = WN * TN * 16;
     static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
+    static_assert(NS == 2 || (NS > 2 && GLDS), "deeper rings are filled by global_load_lds");
     constexpr int Q = BK / 4;        // float4 per image row
     constexpr int RP = 256 / BK;     // image rows per 1 KB global_load_lds piece
     constexpr int A_F4 = BM * Q, B_F4 = BN * Q;
     constexpr int A_IT = (A_F4 + 255) / 256, B_IT = (B_F4 + 255) / 256;
 
-    // one LDS array: [2][BM][BK] A image, then [2][BN][BK] W image
-    __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * BK];
+    // one LDS array: [NS][BM][BK] A image, then [NS][BN][BK] W image
+    __shared__ __attribute__((aligned(16))) float smem[NS * (BM + BN) * BK];
     float (*As)[BM][BK] = reinterpret_cast<float (*)[BM][BK]>(smem);
-    float (*Bs)[BN][BK] = reinterpret_cast<float (*)[BN][BK]>(smem + 2 * BM * BK);
+    float (*Bs)[BN][BK] = reinterpret_cast<float (*)[BN][BK]>(smem + NS * BM * BK);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
@@ -327,6 +335,40 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     f32x4 res[RES_PREFETCH ? TM * TN : 1];
 
     const int nk = p.K / BK;
+    if constexpr (NS > 2) {
+        // NS-deep LDS ring for latency-bound shapes (few blocks, weights streamed from HBM):
+        // NS - 1 k-tiles in flight; counted vmcnt + raw s_barrier so the DMA spans barriers
+        // (__syncthreads would drain every outstanding glds).  Per iteration: wait until tile
+        // kt has landed (this wave's pieces), barrier (everyone's pieces landed, everyone done
+        // with tile kt - 1), refill the slot of tile kt - 1 with tile kt + NS - 1, compute.
+        constexpr int G = (BM / RP + 3) / 4 + (BN / RP + 3) / 4;  // glds per wave per tile
+#pragma unroll
+        for (int i = 0; i < NS - 1; ++i)
+            if (i < nk) glds_tile(i, i * BK);
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + NS - 2 < nk) wait_vmcnt<(NS - 2) * G>();
+            else wait_vmcnt<0>();
+            // this wave's LDS reads of tile kt - 1 are done before anyone refills its slot
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + NS - 1 < nk) glds_tile((kt + NS - 1) % NS, (kt + NS - 1) * BK);
+            if constexpr (RES_PREFETCH) {
+                if (kt == nk - 1) {
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            const int row = m0 + arow0 + i * 16 + frow, col = n0 + brow0 + j * 16 + fk;
+                            res[i * TN + j] = (row < p.M && col < p.N)
+                                                  ? *reinterpret_cast<const f32x4*>(res_at(p, row, col))
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+                        }
+                }
+            }
+            compute(kt % NS);
+        }
+    } else {
     if constexpr (GLDS) {
         glds_tile(0, 0);
     } else {
@@ -361,6 +403,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             }
     }
     compute((nk - 1) & 1);
+    }
 
     // no barrier: each wave finishes its own tile from registers
     float rs[TM];
