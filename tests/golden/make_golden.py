@@ -4,6 +4,7 @@ Run in the build container only (needs /root/reference, read-only; nothing is
 copied from it — only its outputs on synthetic inputs are saved):
 
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py --c5   # Llama-3-shape slice
 
 The reference ships no golden vectors, so these fixtures are
 the parity anchor: the oracle (oracle/llama3_oracle.py) is pinned against them
@@ -133,7 +134,26 @@ def model_fixture(tmp, name, args, hidden, seed, preset, cases, gen=None):
     return out
 
 
+def c5_slice_fixture(tmp):
+    """a 2-layer Llama-3-8B-shaped slice (D 4096, H 32 / KVH 8, HD 128,
+    FD 14336, VS 128256), B = 1: prefill L = 256, then two decode steps at the reference's
+    positions (257, 258: slot 256 is the decode hole).  Only ids and logits are stored; the
+    6 GB weight set is regenerated from the seed (its sha256 is recorded)."""
+    args = synth.llama3_shape(n_layers=2, max_batch_size=1)
+    rng = np.random.default_rng(5)
+    ids = rng.integers(0, args.vocab_size, (1, 256))
+    d1 = rng.integers(0, args.vocab_size, (1, 1))
+    d2 = rng.integers(0, args.vocab_size, (1, 1))
+    model_fixture(tmp, "c5_slice", args, synth.LLAMA3_HIDDEN, 2, "default",
+                  [("prefill", ids, 0), ("dec1", d1, 257), ("dec2", d2, 258)])
+
+
 def main():
+    if "--c5" in sys.argv:  # separate: ~6 GB of weights, about a minute of reference CPU time
+        with tempfile.TemporaryDirectory(dir=os.environ.get("GOLDEN_TMP")) as tmp:
+            c5_slice_fixture(tmp)
+        print("c5 fixture written to", HERE)
+        return
     tokenizer_fixture()
     ops_fixture()
     rng = np.random.default_rng(3)

@@ -380,3 +380,24 @@ def test_cache_edges_full_context_single_token_prompt(tmpdir_mod):
         nxt = want[:, -1, :].argmax(-1)[:, None]
         got, want = m(nxt, pos), ref(nxt, pos)
         _close(got, want)
+
+
+@pytest.mark.timeout(600)
+def test_c5_slice_llama3_shape_against_golden():
+    """2-layer Llama-3-8B shape (D 4096, GQA 32/8, HD 128, FD 14336,
+    VS 128256), B = 1: prefill L = 256 on the MFMA tiles, then decode at positions 257 and 258
+    (GEMV path; slot 256 is the decode hole).  6 GB of weights regenerated from the seed and
+    loaded through the streaming loader (keep_host_weights=False); ids exact, logits 1e-4."""
+    g = load_golden("c5_slice")
+    args = synth.llama3_shape(n_layers=2, max_batch_size=1)
+    with tempfile.TemporaryDirectory() as d:
+        w, path = _model(d, args, synth.LLAMA3_HIDDEN, int(g["seed"]), str(g["preset"]))
+        assert synth.digest(w) == str(g["weights_sha256"])
+        del w
+        m = llama3.Llama(path, args, keep_host_weights=False)
+    for tag in ("prefill", "dec1", "dec2"):
+        out = m(g[f"{tag}_ids"], int(g[f"{tag}_start"]))
+        want = g[f"{tag}_logits"]
+        assert out.shape == want.shape
+        assert _close(out, want) <= 1e-4
+        assert int(out[0, -1].argmax()) == int(want[0, -1].argmax())

@@ -5,6 +5,8 @@ The oracle restates the same NumPy op sequence, so agreement is expected at
 float64 round-off (<= 1e-12), far tighter than the 1e-4 GPU parity bar.
 """
 
+import os
+
 import numpy as np
 import pytest
 
@@ -73,3 +75,16 @@ def test_oracle_greedy_stories_matches_reference(name):
     ids = orc.greedy_ids(m, g["dream_prompt"], int(g["dream_max_new"]))
     np.testing.assert_array_equal(ids, g["dream_ids"])
     assert int(g["dream_zero_slots"][0]) == g["dream_prompt"].shape[1]  # slot L never written
+
+
+@pytest.mark.skipif(not os.environ.get("L3_SLOW_TESTS"),
+                    reason="Llama-3-shape slice: 6 GB of weights, ~1.5 min (set L3_SLOW_TESTS=1)")
+def test_oracle_c5_slice_matches_reference():
+    """2-layer Llama-3-8B shape (GQA n_rep 4, HD 128), B = 1, L = 256
+    prefill then decode at positions 257 and 258 (slot 256 is the decode hole)."""
+    g = load_golden("c5_slice")
+    args = synth.llama3_shape(n_layers=2, max_batch_size=1)
+    m = orc.OracleModel(_weights_for(g, args, synth.LLAMA3_HIDDEN), args)
+    for t in ["prefill", "dec1", "dec2"]:
+        out = m(g[f"{t}_ids"], int(g[f"{t}_start"]))
+        assert np.max(np.abs(out - g[f"{t}_logits"])) <= TIGHT

@@ -35,7 +35,6 @@ struct Variant {
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, dim3(256), 0, s, a); \
             }}
 
-
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
     for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;

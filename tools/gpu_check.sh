@@ -18,6 +18,7 @@ for s in "$@"; do
   case "$s" in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1200 python -m pytest tests -m gpu -q -rf --timeout 600 ;;
+    c5slice) step c5slice 900 python -u -m pytest tests/test_gpu_parity.py -k c5_slice -x -v --timeout 600 --timeout-method thread ;;
     testsx) step tests 1200 python -m pytest tests -m gpu -q -x -rf --timeout 600 ;;
     bench) step bench 600 python bench.py ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown ;;
