@@ -82,6 +82,14 @@ struct Timer {
 struct l3_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // batch split: a large prefill runs as two independent halves of the batch rows on stream
+    // and aux (llama3.py:163-211 never mixes rows), so each half's kernels fill the other's
+    // launch tails and boundaries; fork / join by events
+    static constexpr int MAX_PARTS = 4;
+    hipStream_t aux[MAX_PARTS - 1] = {};
+    hipEvent_t fork_ev = nullptr, join_ev[MAX_PARTS - 1] = {};
+    int split = 2;                   // parts (1 = off); l3_set_batch_split, L3_BATCH_SPLIT
+    int64_t split_min_tokens = 8192; // a part must hold at least this many tokens
     l3_dims d{};
     int HD = 0, qdim = 0, kvdim = 0, qkvn = 0;
     float* emb = nullptr;
@@ -127,7 +135,7 @@ static int set_dev(l3_ctx* c) {
 }
 
 template <typename F>
-static int timed(l3_ctx* c, int kind, F&& launch) {
+static int timed_on(l3_ctx* c, int kind, hipStream_t s, F&& launch) {
     Timer* t = nullptr;
     if (c->timing && (c->timing_mask >> kind & 1u)) {
         if (c->timer_used == c->timers.size()) {
@@ -138,12 +146,17 @@ static int timed(l3_ctx* c, int kind, F&& launch) {
         }
         t = &c->timers[c->timer_used++];
         t->kind = kind;
-        HIP_TRY(hipEventRecord(t->a, c->stream));
+        HIP_TRY(hipEventRecord(t->a, s));
     }
     hipError_t e = launch();
     if (e != hipSuccess) return fail("kernel launch (kind %d) failed: %s", kind, hipGetErrorString(e));
-    if (t) HIP_TRY(hipEventRecord(t->b, c->stream));
+    if (t) HIP_TRY(hipEventRecord(t->b, s));
     return 0;
+}
+
+template <typename F>
+static int timed(l3_ctx* c, int kind, F&& launch) {
+    return timed_on(c, kind, c->stream, launch);
 }
 
 static int harvest_timers(l3_ctx* c) {
@@ -226,14 +239,23 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     l3_ctx* c = new l3_ctx();
     c->device = device;
     c->d = d;
+    if (const char* e = getenv("L3_BATCH_SPLIT")) {  // default for new contexts
+        const int n = atoi(e);
+        c->split = n < 1 ? 1 : n > l3_ctx::MAX_PARTS ? l3_ctx::MAX_PARTS : n;
+    }
     c->HD = HD;
     c->qdim = d.n_heads * HD;
     c->kvdim = d.n_kv_heads * HD;
     c->qkvn = c->qdim + 2 * c->kvdim;
     auto bail = [&](int rc) { l3_destroy(c); return rc; };
     if (set_dev(c)) return bail(1);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
-        return bail(fail("hipStreamCreate failed"));
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
+        return bail(fail("hipStreamCreate / hipEventCreate failed"));
+    for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i)
+        if (hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) != hipSuccess)
+            return bail(fail("hipStreamCreate / hipEventCreate failed"));
     c->layers.resize(d.n_layers > 0 ? d.n_layers : 0);
     if (d.n_layers > 0) {
         const int64_t D = d.dim, FD = d.hidden_dim;
@@ -287,6 +309,11 @@ extern "C" int l3_destroy(l3_ctx* c) {
     drop_decode_graph(c);
     dfree(c->dec_ids); dfree(c->dec_pos);
     if (c->dec_host) (void)hipHostFree(c->dec_host);
+    for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i) {
+        if (c->aux[i]) { (void)hipStreamSynchronize(c->aux[i]); (void)hipStreamDestroy(c->aux[i]); }
+        if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
+    }
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -453,70 +480,109 @@ static int check_call(l3_ctx* c, int B, int L, int start_pos) {
 // (llama3.py:287 fused into the QKV GEMM's A gather and the O-proj's residual), so no embed
 // kernel runs and h is first written by that O-proj
 static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* pos_dev = nullptr,
-                     const int32_t* emb_ids = nullptr) {
+                     const int32_t* emb_ids = nullptr, int b0 = 0, hipStream_t s = nullptr) {
+    // rows [b0, b0 + B) of the batch on stream s: every buffer is offset to batch row b0
+    if (!s) s = c->stream;
     Layer& Ly = c->layers[li];
-    const int64_t T = (int64_t)B * L;
+    const int64_t T = (int64_t)B * L, r0 = (int64_t)b0 * L;
     const int D = c->d.dim, FD = c->d.hidden_dim;
+    const int64_t cache0 = (int64_t)b0 * c->d.n_kv_heads * c->d.max_seq_len * c->HD;
+    float* h = c->h + r0 * D;
+    float* q = c->q + r0 * c->qdim;
+    float* attn = c->attn + r0 * c->qdim;
+    float* hid = c->hid + r0 * FD;
+    if (emb_ids) emb_ids += r0;
     GemmArgs g{};
     g.eps = c->d.norm_eps;
     // rmsnorm -> QKV -> RoPE -> q + KV-cache append
-    g.A = c->h; g.lda = D; g.W = Ly.wqkv; g.C = nullptr; g.ldc = 0;
+    g.A = h; g.lda = D; g.W = Ly.wqkv; g.C = nullptr; g.ldc = 0;
     g.M = (int)T; g.N = c->qkvn; g.K = D; g.norm = true;  // n_attn folded into wqkv
-    g.q_out = c->q; g.cache_k = Ly.cache_k; g.cache_v = Ly.cache_v;
+    g.q_out = q; g.cache_k = Ly.cache_k + cache0; g.cache_v = Ly.cache_v + cache0;
     g.rope_cos = c->rope_cos; g.rope_sin = c->rope_sin;
     g.L = L; g.start_pos = start_pos; g.H = c->d.n_heads; g.KVH = c->d.n_kv_heads; g.HD = c->HD;
     g.Smax = c->d.max_seq_len;
     g.pos_dev = pos_dev;
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     if (emb_ids) { g.A = c->emb; g.a_rows = emb_ids; }
-    if (timed(c, L3_K_QKV, [&] { return launch_gemm(EPI_QKV, g, c->stream); })) return 1;
+    if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
     // causal attention over the cache
     AttnArgs a{};
-    a.q = c->q; a.cache_k = Ly.cache_k; a.cache_v = Ly.cache_v; a.out = c->attn;
+    a.q = q; a.cache_k = Ly.cache_k + cache0; a.cache_v = Ly.cache_v + cache0; a.out = attn;
     a.B = B; a.L = L; a.start_pos = start_pos; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
     a.HD = c->HD; a.Smax = c->d.max_seq_len; a.pos_dev = pos_dev;
-    if (timed(c, L3_K_ATTN, [&] { return launch_attention(a, c->stream); })) return 1;
+    if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention(a, s); })) return 1;
     // O-proj + residual (in place on h)
     GemmArgs o{};
-    o.A = c->attn; o.lda = c->qdim; o.W = Ly.wo; o.C = c->h; o.ldc = D;
+    o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.C = h; o.ldc = D;
     o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
     if (emb_ids) { o.res_src = c->emb; o.res_rows = emb_ids; }  // h = emb[ids] + attn . Wo^T
-    if (timed(c, L3_K_OPROJ, [&] { return launch_gemm(EPI_RESID, o, c->stream); })) return 1;
+    if (timed_on(c, L3_K_OPROJ, s, [&] { return launch_gemm(EPI_RESID, o, s); })) return 1;
     // rmsnorm -> gate|up -> SwiGLU
     GemmArgs gu{};
-    gu.A = c->h; gu.lda = D; gu.W = Ly.wgu; gu.C = c->hid; gu.ldc = FD;
+    gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
     gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true;  // n_ffn folded into wgu
     gu.eps = c->d.norm_eps;
-    if (timed(c, L3_K_GATEUP, [&] { return launch_gemm(EPI_SWIGLU, gu, c->stream); })) return 1;
+    if (timed_on(c, L3_K_GATEUP, s, [&] { return launch_gemm(EPI_SWIGLU, gu, s); })) return 1;
     // down + residual
     GemmArgs dn{};
-    dn.A = c->hid; dn.lda = FD; dn.W = Ly.wd; dn.C = c->h; dn.ldc = D;
+    dn.A = hid; dn.lda = FD; dn.W = Ly.wd; dn.C = h; dn.ldc = D;
     dn.M = (int)T; dn.N = D; dn.K = FD; dn.norm = false;
-    if (timed(c, L3_K_DOWN, [&] { return launch_gemm(EPI_RESID, dn, c->stream); })) return 1;
+    if (timed_on(c, L3_K_DOWN, s, [&] { return launch_gemm(EPI_RESID, dn, s); })) return 1;
     return 0;
 }
 
+// final RMSNorm + lm_head on the last position of rows [b0, b0 + B) (llama3.py:304-307)
+static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipStream_t s) {
+    const int64_t D = c->d.dim, VS = c->d.vocab_size;
+    GemmArgs lm{};
+    lm.A = c->h + ((int64_t)b0 * L + L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
+    lm.C = logits_dev + (int64_t)b0 * VS; lm.ldc = VS;
+    lm.M = B; lm.N = (int)VS; lm.K = (int)D; lm.norm = true;  // final norm folded
+    lm.eps = c->d.norm_eps;
+    return timed_on(c, L3_K_LMHEAD, s, [&] { return launch_gemm(EPI_STORE, lm, s); });
+}
+
+// Batch split of a prefill: rows are independent (llama3.py:163-211), so the layers run as
+// c->split row ranges on their own streams and one range's kernels fill another's launch tails
+// and kernel boundaries (C3: 7.31 -> 7.04 ms/step at 2 parts; 3 and 4 parts are slower).
+
 static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
                        float* logits_dev, const int* pos_dev = nullptr) {
-    const int D = c->d.dim;
     // roctx ranges (host-side launch spans; `rocprofv3 --marker-trace`) per block and lm_head
     static const char* names[] = {"l3.layer0", "l3.layer1", "l3.layer2", "l3.layer3", "l3.layer4",
                                   "l3.layer5", "l3.layer6", "l3.layer7", "l3.layerN"};
-    roctxRangePushA("l3.forward");
-    for (int li = 0; li < (int)c->layers.size(); ++li) {
-        roctxRangePushA(names[li < 8 ? li : 8]);
-        const int rc = run_layer(c, li, B, L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr);
-        roctxRangePop();
-        if (rc) { roctxRangePop(); return 1; }
+    // a part keeps more than 256 rows, so every layer GEMM runs the same M-independent MFMA
+    // tiles as the unsplit batch (the row-blocked GEMV of short M rounds by row position)
+    const int64_t min_part = c->split_min_tokens > 256 ? c->split_min_tokens : 257;
+    int parts = pos_dev ? 1 : c->split;
+    while (parts > 1 && (B < parts || (int64_t)(B / parts) * L < min_part)) --parts;
+    int nb[l3_ctx::MAX_PARTS], b0[l3_ctx::MAX_PARTS];
+    hipStream_t st[l3_ctx::MAX_PARTS];
+    for (int p = 0; p < parts; ++p) {
+        b0[p] = (int)((int64_t)B * p / parts);
+        nb[p] = (int)((int64_t)B * (p + 1) / parts) - b0[p];
+        st[p] = p ? c->aux[p - 1] : c->stream;
     }
-    // final RMSNorm + lm_head on the last position of each sequence (llama3.py:304-307)
+    roctxRangePushA("l3.forward");
+    if (parts > 1) {  // the aux streams join the work queued so far on stream
+        HIP_TRY(hipEventRecord(c->fork_ev, c->stream));
+        for (int p = 1; p < parts; ++p) HIP_TRY(hipStreamWaitEvent(st[p], c->fork_ev, 0));
+    }
+    int rc = 0;
+    for (int li = 0; li < (int)c->layers.size() && !rc; ++li) {
+        roctxRangePushA(names[li < 8 ? li : 8]);
+        for (int p = 0; p < parts && !rc; ++p)
+            rc = run_layer(c, li, nb[p], L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr, b0[p], st[p]);
+        roctxRangePop();
+    }
+    for (int p = 1; p < parts; ++p) {  // stream waits for every part: later calls see all rows
+        HIP_TRY(hipEventRecord(c->join_ev[p - 1], st[p]));
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->join_ev[p - 1], 0));
+    }
+    // one lm_head over all B rows (its tile choice depends on M: per-part launches would round
+    // differently from the unsplit batch)
     roctxRangePushA("l3.lm_head");
-    GemmArgs lm{};
-    lm.A = c->h + (int64_t)(L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
-    lm.C = logits_dev; lm.ldc = c->d.vocab_size;
-    lm.M = B; lm.N = c->d.vocab_size; lm.K = D; lm.norm = true;  // final norm folded
-    lm.eps = c->d.norm_eps;
-    const int rc = timed(c, L3_K_LMHEAD, [&] { return launch_gemm(EPI_STORE, lm, c->stream); });
+    if (!rc) rc = run_lm_head(c, B, L, logits_dev, 0, c->stream);
     roctxRangePop();
     roctxRangePop();
     return rc;
@@ -534,6 +600,16 @@ static int upload_ids(l3_ctx* c, const int64_t* ids_host, int64_t T) {
     }
     HIP_TRY(hipMemcpyAsync(c->ids, tmp.data(), T * 4, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));  // tmp goes out of scope
+    return 0;
+}
+
+extern "C" int l3_set_batch_split(l3_ctx* c, int32_t parts, int64_t min_tokens) {
+    CHECK_CTX(c);
+    if (parts < 1 || parts > l3_ctx::MAX_PARTS)
+        return fail("l3_set_batch_split: parts %d outside [1, %d]", parts, l3_ctx::MAX_PARTS);
+    if (min_tokens < 1) return fail("l3_set_batch_split: min_tokens %lld < 1", (long long)min_tokens);
+    c->split = parts;
+    c->split_min_tokens = min_tokens;
     return 0;
 }
 

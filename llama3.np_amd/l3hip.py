@@ -71,6 +71,7 @@ _SIGNATURES = {
     "l3_h2d": (ctypes.c_int, [_P, _P, _P, _SZ]),
     "l3_d2h": (ctypes.c_int, [_P, _P, _P, _SZ]),
     "l3_synchronize": (ctypes.c_int, [_P]),
+    "l3_set_batch_split": (ctypes.c_int, [_P, _I32, _I64]),
     "l3_kernel_timing": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
     "l3_comm_unique_id": (ctypes.c_int, [_P]),
@@ -222,6 +223,11 @@ class Context:
 
     def forward_dev(self, ids_dev: int, B: int, L: int, start_pos: int, logits_dev: int) -> None:
         check(lib().l3_forward_dev(self._h, ids_dev, B, L, start_pos, logits_dev))
+
+    def set_batch_split(self, parts: int, min_tokens: int = 8192) -> None:
+        """Run a model forward as `parts` batch-row ranges on their own streams (extension;
+        results bit-identical for any split, default 2)."""
+        check(lib().l3_set_batch_split(self._h, int(parts), int(min_tokens)))
 
     def synchronize(self) -> None:
         check(lib().l3_synchronize(self._h))

@@ -108,6 +108,17 @@ int main(void) {
             fprintf(stderr, "FAIL non-finite logit at %d\n", i);
             return 1;
         }
+    // batch split API (parts of 9 tokens stay unsplit: a part needs > 256 rows)
+    float* logits2 = (float*)malloc(sizeof(float) * B * VS);
+    EXPECT_FAIL(l3_set_batch_split(c, 0, 1));
+    CHECK(l3_set_batch_split(c, 2, 1));
+    CHECK(l3_forward_host(c, ids, B, L, 0, logits2));
+    if (memcmp(logits, logits2, sizeof(float) * B * VS) != 0) {
+        fprintf(stderr, "FAIL batch split changed the logits\n");
+        return 1;
+    }
+    free(logits2);
+    CHECK(l3_set_batch_split(c, 1, 1));
     int64_t nxt[B];
     CHECK(l3_greedy_step_host(c, ids, B, L, 0, nxt, NULL));
     for (int b = 0; b < B; ++b)

@@ -253,6 +253,33 @@ def test_full_size_batch_rows_independent_and_match_oracle(tmpdir_mod):
         assert _close(full[r:r + 1], ref(ids[r:r + 1], 0)) <= 1e-4
 
 
+def test_batch_split_bit_identical(tmpdir_mod):
+    """The batch split (row ranges on concurrent streams, l3_set_batch_split) changes only
+    which stream runs a row: logits bit-identical for 1-4 parts, uneven parts included
+    (B = 63), on a prefill, a chunk at start_pos > 0 and through the greedy step."""
+    args = synth.stories15m(63)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    m = llama3.Llama(path, args)
+    ctx = m.context
+    rng = np.random.default_rng(12)
+    a = rng.integers(0, args.vocab_size, (63, 200))
+    b = rng.integers(0, args.vocab_size, (63, 40))
+    outs = []
+    for parts in (1, 2, 3, 4):
+        ctx.set_batch_split(parts, min_tokens=1)
+        la = m(a, 0)
+        lb = m(b, 200)
+        nxt, _ = ctx.greedy_step(b, 200)
+        outs.append((la, lb, nxt))
+    for la, lb, nxt in outs[1:]:
+        np.testing.assert_array_equal(la, outs[0][0])
+        np.testing.assert_array_equal(lb, outs[0][1])
+        np.testing.assert_array_equal(nxt, outs[0][2])
+    with pytest.raises(RuntimeError, match="outside"):
+        ctx.set_batch_split(5)
+    ctx.set_batch_split(2)
+
+
 # ---- decode state / graph replay ------------------------------------------------------------
 
 def test_generate_twice_and_off_schedule_steps_match_oracle(tmpdir_mod):

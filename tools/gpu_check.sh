@@ -21,6 +21,8 @@ for s in "$@"; do
     c5slice) step c5slice 900 python -u -m pytest tests/test_gpu_parity.py -k c5_slice -x -v --timeout 600 --timeout-method thread ;;
     testsx) step tests 1200 python -m pytest tests -m gpu -q -x -rf --timeout 600 ;;
     bench) step bench 600 python bench.py ;;
+    benchq) step benchq 300 python bench.py --no-cpu-baseline ;;
+    split[1-4]) L3_BATCH_SPLIT=${s#split} step $s 300 python bench.py --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown ;;

@@ -1,10 +1,14 @@
 """Summarise a rocprofv3 --kernel-trace --stats run into profiles/ (tracked).
 
     python tools/rocprof_summary.py gpurun_out/prof/run_kernel_stats.csv profiles/r01_c3 \
-        --rows 65536 [--bench gpurun_out/bench.log]
+        --rows 65536 [--bench gpurun_out/bench.log] [--trace gpurun_out/prof/run_kernel_trace.csv]
 
 Writes <prefix>_kernel_stats.csv (the raw rocprofv3 summary) and <prefix>_summary.md with
-per-kernel calls, mean duration and algorithmic TFLOP/s at the stories15M C3 shape.
+per-kernel calls, mean duration and algorithmic TFLOP/s at the stories15M C3 shape.  With
+--trace the rows are per (kernel, grid) from the dispatch trace: bench.py's timed forward runs
+the batch as two row ranges on concurrent streams (half-size grids, sharing the CUs) and its
+roofline pass serialized (full grids, the kernel alone), so the two are reported apart; a
+dispatch's rows are --rows x its grid / the kernel's largest grid.
 """
 import argparse
 import csv
@@ -37,16 +41,37 @@ def main():
     ap.add_argument("prefix")
     ap.add_argument("--rows", type=int, default=65536)
     ap.add_argument("--bench")
+    ap.add_argument("--trace")
     a = ap.parse_args()
     shutil.copy(a.stats, a.prefix + "_kernel_stats.csv")
-    lines = ["| kernel | role | calls | mean µs | algorithmic TFLOP/s | % of 157.3 |", "|---|---|---|---|---|---|"]
-    with open(a.stats) as f:
-        for r in csv.DictReader(f):
-            role, fl = flops(r["Name"], a.rows)
-            us = float(r["AverageNs"]) / 1e3
-            tf = f"{fl / (us * 1e-6) / 1e12:.1f}" if fl else "-"
-            pc = f"{fl / (us * 1e-6) / 1e12 / 157.3 * 100:.1f}" if fl else "-"
-            lines.append(f"| `{r['Name'][:60]}` | {role} | {r['Calls']} | {us:.1f} | {tf} | {pc} |")
+    lines = ["| kernel | role | grid | calls | mean µs | algorithmic TFLOP/s | % of 157.3 |",
+             "|---|---|---|---|---|---|---|"]
+    rows = []  # (name, grid, calls, mean ns, total ns)
+    if a.trace:
+        groups = {}
+        with open(a.trace) as f:
+            for r in csv.DictReader(f):
+                g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+                d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                groups.setdefault((r["Kernel_Name"], g), []).append(d)
+        for (name, g), ds in groups.items():
+            rows.append((name, g, len(ds), sum(ds) / len(ds), sum(ds)))
+    else:
+        with open(a.stats) as f:
+            for r in csv.DictReader(f):
+                rows.append((r["Name"], None, int(r["Calls"]), float(r["AverageNs"]), float(r["TotalDurationNs"])))
+    gmax = {}
+    for name, g, *_ in rows:
+        if g:
+            gmax[name] = max(gmax.get(name, 0), g)
+    for name, g, calls, ns, _ in sorted(rows, key=lambda x: -x[4]):
+        t = a.rows * g // gmax[name] if g else a.rows
+        role, fl = flops(name, t)
+        us = ns / 1e3
+        tf = f"{fl / (us * 1e-6) / 1e12:.1f}" if fl else "-"
+        pc = f"{fl / (us * 1e-6) / 1e12 / 157.3 * 100:.1f}" if fl else "-"
+        gs = f"{g} ({t} rows)" if g else "-"
+        lines.append(f"| `{name[:60]}` | {role} | {gs} | {calls} | {us:.1f} | {tf} | {pc} |")
     if a.bench:
         for line in open(a.bench):
             if line.startswith("{"):
