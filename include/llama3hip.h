@@ -105,7 +105,8 @@ int l3_forward_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
  * lm_head on the context stream.  Rows never interact (llama3.py:163-211) and every part keeps
  * the unsplit batch's kernels, so the results are bit-identical for any split; one part's
  * kernels fill another's launch tails.  A forward uses fewer parts when a part would hold fewer
- * than max(min_tokens, 257) tokens (B*L/parts), and one part for graph-captured decode steps.
+ * than max(min_tokens, 257) tokens (B*L/parts), one part when a layer exceeds 1 TFLOP (long
+ * kernels: no tails to fill) and one part for graph-captured decode steps.
  * parts in [1, 4], min_tokens >= 1 (default 8192). */
 int l3_set_batch_split(l3_ctx* ctx, int32_t parts, int64_t min_tokens);
 /* Same with device-resident ids (int32 [B, L]) and logits ([B, VS]); async. */

@@ -554,7 +554,11 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
     // a part keeps more than 256 rows, so every layer GEMM runs the same M-independent MFMA
     // tiles as the unsplit batch (the row-blocked GEMV of short M rounds by row position)
     const int64_t min_part = c->split_min_tokens > 256 ? c->split_min_tokens : 257;
-    int parts = pos_dev ? 1 : c->split;
+    // ... and only while a layer is short enough for launch tails to matter: past ~1 TFLOP per
+    // layer (C5, Llama-3-8B shape: 57 TFLOP) the split measured -0.8 %, at C3 (0.12) +3.9 %
+    const double D = c->d.dim, layer_flops = 2.0 * B * L *
+        (D * c->qkvn + D * c->qdim + 3.0 * D * c->d.hidden_dim);
+    int parts = pos_dev || layer_flops > 1e12 ? 1 : c->split;
     while (parts > 1 && (B < parts || (int64_t)(B / parts) * L < min_part)) --parts;
     int nb[l3_ctx::MAX_PARTS], b0[l3_ctx::MAX_PARTS];
     hipStream_t st[l3_ctx::MAX_PARTS];

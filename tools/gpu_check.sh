@@ -37,6 +37,7 @@ for s in "$@"; do
     decode) step decode 300 python tools/bench_decode.py ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
     c5small) step c5small 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
+    c5small1) L3_BATCH_SPLIT=1 step c5small1 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
     rccl1) step rccl1 180 python tools/rccl_selftest.py --world 1 ;;
     torchrun1) step torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline ;;
