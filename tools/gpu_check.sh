@@ -18,7 +18,7 @@ for s in "$@"; do
   case "$s" in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) step tests 1200 python -m pytest tests -m gpu -q -rf --timeout 600 ;;
-    c5slice) step c5slice 900 python -u -m pytest tests/test_gpu_parity.py -k c5_slice -x -v --timeout 600 --timeout-method thread ;;
+    c5slice) step c5slice 900 python -u -m pytest tests/test_gpu_parity.py -k c5_ -x -v --timeout 900 --timeout-method thread ;;
     testsx) step tests 1200 python -m pytest tests -m gpu -q -x -rf --timeout 600 ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --no-cpu-baseline ;;
