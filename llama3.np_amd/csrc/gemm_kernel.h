@@ -479,6 +479,38 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     // row block: rows [m0, m0 + Mb) of A (grid.y row blocks of MR rows re-read W through L2)
     const int m0 = blockIdx.y * MR, Mb = min(MR, p.M - m0);
     load_chunk(0);  // in flight while the input rows are staged
+    // the epilogue's own operands (EPI_RESID: the residual; EPI_QKV: the RoPE cos / sin of the
+    // pair) do not depend on the dot products: fetch them now, not after the reduction (one
+    // memory round trip less per launch; decode runs three such launches per layer)
+    const bool writer = j == 0 && valid;
+    float pre0[MR], pre1[MR];
+    int qkv_sec = 0, qkv_head = 0, qkv_d = 0;  // EPI_QKV: 0 q, 1 k, 2 v; head; column in head
+    if constexpr (EPI == EPI_QKV) {
+        const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD, col = 2 * u;
+        qkv_sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
+        const int cc = col - (qkv_sec == 0 ? 0 : qkv_sec == 1 ? qdim : qdim + kvdim);
+        qkv_head = cc / p.HD;
+        qkv_d = cc - qkv_head * p.HD;
+    }
+#pragma unroll
+    for (int mi = 0; mi < MR; ++mi) {
+        pre0[mi] = 0.f;
+        pre1[mi] = 0.f;
+        if (!writer || mi >= Mb) continue;
+        const int m = m0 + mi;
+        if constexpr (EPI == EPI_RESID) {
+            pre0[mi] = *res_at(p, m, unit);
+        } else if constexpr (EPI == EPI_QKV) {
+            if (qkv_sec < 2) {
+                const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
+                const int t = pos * (p.HD >> 1) + (qkv_d >> 1);
+                pre0[mi] = p.rope_cos[t];
+                pre1[mi] = p.rope_sin[t];
+            } else {
+                pre0[mi] = 1.f;  // V: identity rotation
+            }
+        }
+    }
     // stage the row block (rows past Mb zero: branch-free FMA loop), SU loads in flight per
     // thread before the first LDS store (a serial load -> store walk costs a round trip each)
     constexpr int SU = 8;
@@ -532,36 +564,30 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) acc[r][m] += __shfl_xor(acc[r][m], o);
         }
-    if (j != 0 || !valid) return;
+    if (!writer) return;
 #pragma unroll
     for (int mi = 0; mi < MR; ++mi) {
         if (mi >= Mb) break;
         const int m = m0 + mi;  // global row
         const float sc = p.norm ? 1.0f / sqrtf(ss[mi] / (float)p.K + p.eps) : 1.0f;
         if constexpr (EPI == EPI_QKV) {
-            // columns 2u, 2u + 1: one RoPE pair (llama3.py:41-76), then q / KV-cache append
-            const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
+            // columns 2u, 2u + 1: one RoPE pair (llama3.py:41-76; V rotates by cos 1, sin 0,
+            // exact), then q / KV-cache append
+            const int qdim = p.H * p.HD;
             const int col = 2 * unit;
-            float v0 = acc[0][mi] * sc, v1 = acc[ROWS - 1][mi] * sc;
+            const float v0 = acc[0][mi] * sc, v1 = acc[ROWS - 1][mi] * sc;
+            const float cs = pre0[mi], sn = pre1[mi];
+            const float r0 = v0 * cs - v1 * sn, r1 = v0 * sn + v1 * cs;
             const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
-            const bool is_q = col < qdim, is_k = !is_q && col < qdim + kvdim;
-            const int cc = is_q ? col : col - qdim - (is_k ? 0 : kvdim);
-            const int head = cc / p.HD, d = cc - head * p.HD;
-            if (is_q || is_k) {
-                const int t = pos * (p.HD >> 1) + (d >> 1);
-                const float cs = p.rope_cos[t], sn = p.rope_sin[t];
-                const float r0 = v0 * cs - v1 * sn, r1 = v0 * sn + v1 * cs;
-                v0 = r0;
-                v1 = r1;
-            }
-            float2* dst = is_q ? reinterpret_cast<float2*>(p.q_out + (int64_t)m * qdim + col)
-                               : reinterpret_cast<float2*>((is_k ? p.cache_k : p.cache_v) +
-                                                           (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d);
-            *dst = is_q ? float2{v0 * p.q_scale, v1 * p.q_scale} : float2{v0, v1};
+            float2* dst = qkv_sec == 0
+                              ? reinterpret_cast<float2*>(p.q_out + (int64_t)m * qdim + col)
+                              : reinterpret_cast<float2*>((qkv_sec == 1 ? p.cache_k : p.cache_v) +
+                                                          (((int64_t)bidx * p.KVH + qkv_head) * p.Smax + pos) * p.HD + qkv_d);
+            *dst = qkv_sec == 0 ? float2{r0 * p.q_scale, r1 * p.q_scale} : float2{r0, r1};
         } else {
             float* dst = p.C + (int64_t)m * p.ldc + unit;
             if constexpr (EPI == EPI_SWIGLU) *dst = silu_f(acc[0][mi] * sc) * (acc[ROWS - 1][mi] * sc);
-            else if constexpr (EPI == EPI_RESID) *dst = *res_at(p, m, unit) + acc[0][mi];
+            else if constexpr (EPI == EPI_RESID) *dst = pre0[mi] + acc[0][mi];
             else *dst = acc[0][mi] * sc;
         }
     }
