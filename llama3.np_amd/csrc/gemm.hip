@@ -48,8 +48,6 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
     if (a.M <= 1 || cap == 1 || (small_w && a.M <= 8)) return launch_gemv_mr<EPI, 1>(a, s);
     if (a.M <= 2 || cap == 2) return launch_gemv_mr<EPI, 2>(a, s);
     if (a.M <= 4 || cap == 4) return launch_gemv_mr<EPI, 4>(a, s);
-    if (a.M <= 2) return launch_gemv_mr<EPI, 2>(a, s);
-    if (a.M <= 4) return launch_gemv_mr<EPI, 4>(a, s);
     return launch_gemv_mr<EPI, 8>(a, s);
 }
 
