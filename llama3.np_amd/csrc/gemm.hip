@@ -51,6 +51,12 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
     return launch_gemv_mr<EPI, 8>(a, s);
 }
 
+bool gemm_is_gemv(const GemmArgs& a) {
+    const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
+    const bool short_m = a.M <= 8 || (a.M <= 256 && (int64_t)a.N * a.K <= (int64_t)4 << 20);
+    return short_m && (size_t)mr * a.K <= 16384;  // A rows fit 64 KB of LDS (QKV: N even)
+}
+
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return hipSuccess;
     if (a.K % 32 != 0 || a.K <= 0) return hipErrorInvalidValue;  // whole 32-deep k-tiles
@@ -60,9 +66,7 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     // epilogues, 8-row blocks beyond M = 8 re-reading W through L2 — for the layer weights up
     // to M = 256 (a 128-row MFMA tile there is one k-loop of memory round trips on a handful of
     // blocks); the 37 MB lm_head keeps the MFMA tiles past M = 8
-    const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
-    const bool short_m = a.M <= 8 || (a.M <= 256 && (int64_t)a.N * a.K <= (int64_t)4 << 20);
-    if (short_m && (size_t)mr * a.K <= 16384) {  // A rows fit 64 KB of LDS (QKV: N even)
+    if (gemm_is_gemv(a)) {
         switch (epi) {
             case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);
             case EPI_QKV: return launch_gemv<EPI_QKV>(a, s);

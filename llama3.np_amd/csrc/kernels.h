@@ -36,6 +36,17 @@ struct GemmArgs {
     const float* res_src; const int32_t* res_rows;
 };
 
+// Device-resident state of the greedy decode loop (graph replay).  pos is first, so &st->pos
+// is the pos_dev the captured kernels read.
+struct DecState {
+    int pos;           // start_pos of the next decode step; the argmax advances it
+    int hist_base;     // generate loop: the ids of the step at position q go to
+    int hist_cap;      //   hist[(q - hist_base) * B + b] while 0 <= q - hist_base < hist_cap
+    unsigned arrive;   // argmax_kernel's block arrival count (0 between launches)
+    int32_t* hist;     // null: no history
+};
+
+
 // row r of A (identity, or the gathered embedding row)
 __device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
     return p.A + (p.a_rows ? (int64_t)p.a_rows[r] : r) * p.lda;
@@ -63,7 +74,9 @@ __device__ __forceinline__ int start_of(const Args& p) {
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
-                         int* pos_dev = nullptr);
+                         DecState* st = nullptr);
+// true when launch_gemm runs this shape on the row-blocked GEMV (short M)
+bool gemm_is_gemv(const GemmArgs& a);
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s);
 hipError_t launch_silu(const float* x, float* y, int64_t n, hipStream_t s);
 hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows, int dim,

@@ -31,7 +31,7 @@ __device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi) 
 
 __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ x, int n,
                                                       int32_t* __restrict__ out,
-                                                      int* __restrict__ pos_dev) {
+                                                      DecState* __restrict__ st) {
     constexpr int NT = 1024, U = 8;
     const float* row = x + (int64_t)blockIdx.x * n;
     const int tid = threadIdx.x;
@@ -80,8 +80,19 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
         }
         if (tid == 0) {
             out[blockIdx.x] = bi;
-            // captured decode step: the next step runs one position later (llama3.py:312-318)
-            if (pos_dev && blockIdx.x == 0) *pos_dev += 1;
+            if (st) {
+                // captured decode step: record the id in the generate history, and the last row
+                // to arrive moves the loop one position on (llama3.py:312-318).  Every block
+                // reads pos before its arrival (the fence orders the read and the history store
+                // before the atomic), so none sees the advanced value.
+                const int pos = st->pos, q = pos - st->hist_base;
+                if (st->hist && q >= 0 && q < st->hist_cap) st->hist[(int64_t)q * gridDim.x + blockIdx.x] = bi;
+                __threadfence();
+                if (atomicAdd(&st->arrive, 1u) == gridDim.x - 1) {
+                    st->arrive = 0u;
+                    st->pos = pos + 1;
+                }
+            }
         }
     }
 }
@@ -152,11 +163,10 @@ static inline unsigned grid_for(int64_t n, int block) {
 }
 
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
-                         int* pos_dev) {
-    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(1024), 0, s, logits, n, out, pos_dev);
+                         DecState* st) {
+    hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(1024), 0, s, logits, n, out, st);
     return hipGetLastError();
 }
-
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s) {
     hipLaunchKernelGGL(softmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, y, rows,
                        n);

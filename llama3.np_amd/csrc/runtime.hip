@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -118,7 +119,8 @@ struct l3_ctx {
     int nranks = 1, rank = 0;
     // captured greedy decode step (llama3.py:316-320 as one hipGraph replay per token)
     int32_t* dec_ids = nullptr;      // [maxB] input ids of the next decode step (argmax output)
-    int* dec_pos = nullptr;          // start_pos of the next decode step (argmax advances it)
+    DecState* dec_state = nullptr;   // device loop state: position, generate history
+    int* dec_pos = nullptr;          // &dec_state->pos: start_pos of the next decode step
     int32_t* dec_host = nullptr;     // pinned [maxB] for the per-token ids copy-back
     hipGraph_t dec_graph = nullptr;
     hipGraphExec_t dec_exec = nullptr;
@@ -307,7 +309,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     for (void* p : c->scratch) dfree(p);
     for (auto& t : c->timers) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     drop_decode_graph(c);
-    dfree(c->dec_ids); dfree(c->dec_pos);
+    dfree(c->dec_ids); dfree(c->dec_state);
     if (c->dec_host) (void)hipHostFree(c->dec_host);
     for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i) {
         if (c->aux[i]) { (void)hipStreamSynchronize(c->aux[i]); (void)hipStreamDestroy(c->aux[i]); }
@@ -532,15 +534,21 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
 }
 
 // final RMSNorm + lm_head on the last position of rows [b0, b0 + B) (llama3.py:304-307)
-static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipStream_t s) {
+static GemmArgs lm_head_args(l3_ctx* c, int B, int L, float* logits_dev, int b0) {
     const int64_t D = c->d.dim, VS = c->d.vocab_size;
     GemmArgs lm{};
     lm.A = c->h + ((int64_t)b0 * L + L - 1) * D; lm.lda = (int64_t)L * D; lm.W = c->lm_head;
     lm.C = logits_dev + (int64_t)b0 * VS; lm.ldc = VS;
     lm.M = B; lm.N = (int)VS; lm.K = (int)D; lm.norm = true;  // final norm folded
     lm.eps = c->d.norm_eps;
+    return lm;
+}
+
+static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipStream_t s) {
+    const GemmArgs lm = lm_head_args(c, B, L, logits_dev, b0);
     return timed_on(c, L3_K_LMHEAD, s, [&] { return launch_gemm(EPI_STORE, lm, s); });
 }
+
 
 // Batch split of a prefill: rows are independent (llama3.py:163-211), so the layers run as
 // c->split row ranges on their own streams and one range's kernels fill another's launch tails
@@ -645,7 +653,7 @@ static int capture_decode_graph(l3_ctx* c, int B) {
     HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
     if (!rc) {
-        hipError_t e = launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, c->dec_pos);
+        hipError_t e = launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, c->dec_state);
         if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
     }
     hipGraph_t g = nullptr;
@@ -666,7 +674,9 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
     if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
     if (!c->dec_ids) {
         HIP_TRY(hipMalloc(&c->dec_ids, (size_t)c->d.max_batch_size * 4));
-        HIP_TRY(hipMalloc(&c->dec_pos, sizeof(int)));
+        HIP_TRY(hipMalloc(&c->dec_state, sizeof(DecState)));
+        HIP_TRY(hipMemset(c->dec_state, 0, sizeof(DecState)));
+        c->dec_pos = &c->dec_state->pos;
         HIP_TRY(hipHostMalloc(&c->dec_host, (size_t)c->d.max_batch_size * 4));
     }
     // Graph replay when this call continues the device-resident decode state: one token per
@@ -732,17 +742,34 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
     if (l3_greedy_step_host(c, first.data(), B, 1, L + 1, nxt.data(), nullptr)) return 1;
     int32_t* hist = nullptr;
     HIP_TRY(hipMalloc(&hist, (size_t)steps * B * 4));
-    auto done = [&](int rc) { (void)hipStreamSynchronize(c->stream); (void)hipFree(hist); return rc; };
+    // the captured argmax writes each replayed step's ids straight into hist (DecState: the
+    // step at position L + i is row i), so the loop is graph launches only
+    auto set_hist = [&](int32_t* ptr, int base, int cap) {
+        DecState h{};
+        h.hist_base = base;
+        h.hist_cap = cap;
+        h.hist = ptr;
+        const size_t off = offsetof(DecState, hist_base);
+        if (hipMemcpyAsync(reinterpret_cast<char*>(c->dec_state) + off, reinterpret_cast<char*>(&h) + off,
+                           sizeof(DecState) - off, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            return false;
+        return hipStreamSynchronize(c->stream) == hipSuccess;  // h is on this stack frame
+    };
+    auto done = [&](int rc) {
+        (void)set_hist(nullptr, 0, 0);
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipFree(hist);
+        return rc;
+    };
     std::vector<int32_t> h32((size_t)B);
     for (int b = 0; b < B; ++b) h32[(size_t)b] = (int32_t)first[(size_t)b];
     if (hipMemcpy(hist, h32.data(), (size_t)B * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpyAsync(hist + B, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
         return done(fail("generate: history copy failed"));
+    if (steps > 2 && !set_hist(hist, L, steps)) return done(fail("generate: decode state update failed"));
     for (int i = 2; i < steps; ++i) {
         if (!c->dec_exec || c->dec_B != B) return done(fail("generate: decode graph not armed"));
-        if (hipGraphLaunch(c->dec_exec, c->stream) != hipSuccess ||
-            hipMemcpyAsync(hist + (size_t)i * B, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToDevice,
-                           c->stream) != hipSuccess)
+        if (hipGraphLaunch(c->dec_exec, c->stream) != hipSuccess)
             return done(fail("generate: graph replay failed"));
         c->graph_steps++;
     }

@@ -282,6 +282,35 @@ def test_batch_split_bit_identical(tmpdir_mod):
 
 # ---- decode state / graph replay ------------------------------------------------------------
 
+@pytest.mark.parametrize("case", ["all_equal", "pair_tie_zero_rest", "nan_rows"])
+def test_decode_argmax_ties_nan(tmpdir_mod, case):
+    """np.argmax's tie-break (first index; -0 == +0; the first NaN wins) through the decode
+    path — eager steps, graph replays, and the device loop whose captured argmax writes each
+    step's ids straight into the generate history (DecState) — against the oracle."""
+    args = synth.tiny(2)
+    w = synth.make_weights(args, synth.TINY_HIDDEN, seed=13, preset="sharp")
+    lm = w["lm_head.weight"]
+    if case == "all_equal":
+        lm[:] = lm[5]                       # every logit equal -> 0
+    elif case == "pair_tie_zero_rest":
+        row = lm[7].copy()
+        lm[:] = 0.0                         # zeros (+0 / -0 sums) tie at column 0
+        lm[7] = row
+        lm[300] = row                       # exact tie 7 / 300 -> 7 when positive
+    else:
+        lm[37] = np.nan
+        lm[200] = np.nan                    # first NaN -> 37
+    path = os.path.join(tmpdir_mod, f"argmax_{case}.npz")
+    synth.save_npz(path, w)
+    prompt = np.random.default_rng(3).integers(0, args.vocab_size, (2, 5))
+    want = orc.greedy_ids(orc.OracleModel(w, args), prompt, 20)
+    m = llama3.Llama(path, args)
+    got = np.concatenate(list(m.generate(prompt, 20)), axis=1)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(m.generate_all(prompt, 20), want)
+    if case == "nan_rows":
+        assert (want == 37).all()
+
 def test_generate_twice_and_off_schedule_steps_match_oracle(tmpdir_mod):
     """Two generate() calls on one model (caches persist, the decode graph is re-armed), then
     greedy steps whose positions break the generate schedule (graph must not replay) — ids
