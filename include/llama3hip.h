@@ -101,10 +101,11 @@ int l3_reset_cache(l3_ctx* ctx);
 int l3_forward_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
                     int32_t start_pos, float* logits_host);
 /* Batch split of a model forward (extension; default 2 parts, env L3_BATCH_SPLIT): the layers
- * run on `parts` contiguous ranges of the B rows, each on its own HIP stream, joined before the
- * lm_head on the context stream.  Rows never interact (llama3.py:163-211) and every part keeps
- * the unsplit batch's kernels, so the results are bit-identical for any split; one part's
- * kernels fill another's launch tails.  A forward uses fewer parts when a part would hold fewer
+ * run on `parts` contiguous ranges of the B rows, each on its own HIP stream, joined on the
+ * context stream before the call returns; the lm_head runs per part when every part picks the
+ * batch's lm_head tile, else once after the join.  Rows never interact (llama3.py:163-211) and
+ * every part keeps the unsplit batch's kernels, so the results are bit-identical for any split;
+ * one part's kernels fill another's launch tails.  A forward uses fewer parts when a part would hold fewer
  * than max(min_tokens, 257) tokens (B*L/parts), one part when a layer exceeds 1 TFLOP (long
  * kernels: no tails to fill) and one part for graph-captured decode steps.
  * parts in [1, 4], min_tokens >= 1 (default 8192). */

@@ -57,6 +57,11 @@ bool gemm_is_gemv(const GemmArgs& a) {
     return short_m && (size_t)mr * a.K <= 16384;  // A rows fit 64 KB of LDS (QKV: N even)
 }
 
+int gemm_store_config(const GemmArgs& a) {
+    if (gemm_is_gemv(a)) return 0;
+    return a.M <= 32 ? 1 : a.M <= 64 ? 2 : 3;
+}
+
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.M <= 0 || a.N <= 0) return hipSuccess;
     if (a.K % 32 != 0 || a.K <= 0) return hipErrorInvalidValue;  // whole 32-deep k-tiles
@@ -94,9 +99,11 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
             return launch<EPI_RESID, 2, 2, 4, 4, 2, 32>(a, s);                   // 128 x 128
         case EPI_STORE:   // lm_head (the 37 MB W streams from HBM past few blocks: deep
                           // LDS rings, B = 64 lm_head 30.3 -> 18.4 us), op-level linear
-            if (a.M <= 32) return launch<EPI_STORE, 2, 2, 1, 4, 2, 16, 6>(a, s);
-            if (a.M <= 64) return launch<EPI_STORE, 2, 2, 2, 4, 2, 16, 6>(a, s);
-            return launch<EPI_STORE, 2, 2, 4, 4, 2, 16, 4>(a, s);
+            switch (gemm_store_config(a)) {
+                case 1: return launch<EPI_STORE, 2, 2, 1, 4, 2, 16, 6>(a, s);
+                case 2: return launch<EPI_STORE, 2, 2, 2, 4, 2, 16, 6>(a, s);
+                default: return launch<EPI_STORE, 2, 2, 4, 4, 2, 16, 4>(a, s);
+            }
         default:
             return hipErrorInvalidValue;
     }

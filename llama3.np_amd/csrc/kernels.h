@@ -77,6 +77,9 @@ hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out,
                          DecState* st = nullptr);
 // true when launch_gemm runs this shape on the row-blocked GEMV (short M)
 bool gemm_is_gemv(const GemmArgs& a);
+// which EPI_STORE kernel launch_gemm picks (0 = GEMV): launches of equal id round identically
+// row by row, whatever their M
+int gemm_store_config(const GemmArgs& a);
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s);
 hipError_t launch_silu(const float* x, float* y, int64_t n, hipStream_t s);
 hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows, int dim,

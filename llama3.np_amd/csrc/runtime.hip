@@ -580,6 +580,12 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
         HIP_TRY(hipEventRecord(c->fork_ev, c->stream));
         for (int p = 1; p < parts; ++p) HIP_TRY(hipStreamWaitEvent(st[p], c->fork_ev, 0));
     }
+    // the lm_head too runs per part when every part picks the unsplit batch's tile (then each
+    // part's lm_head overlaps the other parts' last layer); otherwise once after the join
+    bool lm_parts = parts > 1;
+    const int lm_cfg = gemm_store_config(lm_head_args(c, B, L, logits_dev, 0));
+    for (int p = 0; p < parts && lm_parts; ++p)
+        lm_parts = gemm_store_config(lm_head_args(c, nb[p], L, logits_dev, b0[p])) == lm_cfg;
     int rc = 0;
     for (int li = 0; li < (int)c->layers.size() && !rc; ++li) {
         roctxRangePushA(names[li < 8 ? li : 8]);
@@ -587,14 +593,15 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
             rc = run_layer(c, li, nb[p], L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr, b0[p], st[p]);
         roctxRangePop();
     }
+    roctxRangePushA("l3.lm_head");
+    for (int p = 0; p < parts && lm_parts && !rc; ++p) rc = run_lm_head(c, nb[p], L, logits_dev, b0[p], st[p]);
+    roctxRangePop();
     for (int p = 1; p < parts; ++p) {  // stream waits for every part: later calls see all rows
         HIP_TRY(hipEventRecord(c->join_ev[p - 1], st[p]));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->join_ev[p - 1], 0));
     }
-    // one lm_head over all B rows (its tile choice depends on M: per-part launches would round
-    // differently from the unsplit batch)
     roctxRangePushA("l3.lm_head");
-    if (!rc) rc = run_lm_head(c, B, L, logits_dev, 0, c->stream);
+    if (!rc && !lm_parts) rc = run_lm_head(c, B, L, logits_dev, 0, c->stream);
     roctxRangePop();
     roctxRangePop();
     return rc;

@@ -253,17 +253,20 @@ def test_full_size_batch_rows_independent_and_match_oracle(tmpdir_mod):
         assert _close(full[r:r + 1], ref(ids[r:r + 1], 0)) <= 1e-4
 
 
-def test_batch_split_bit_identical(tmpdir_mod):
+@pytest.mark.parametrize("B", [63, 160])
+def test_batch_split_bit_identical(tmpdir_mod, B):
     """The batch split (row ranges on concurrent streams, l3_set_batch_split) changes only
-    which stream runs a row: logits bit-identical for 1-4 parts, uneven parts included
-    (B = 63), on a prefill, a chunk at start_pos > 0 and through the greedy step."""
-    args = synth.stories15m(63)
+    which stream runs a row: logits bit-identical for 1-4 parts, uneven parts included, on a
+    prefill, a chunk at start_pos > 0 and through the greedy step.  B = 63: the parts' lm_head
+    tile differs from the batch's, so it runs once after the join; B = 160: every part keeps
+    the batch's lm_head tile and runs its own on its stream."""
+    args = synth.stories15m(B)
     _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
     m = llama3.Llama(path, args)
     ctx = m.context
     rng = np.random.default_rng(12)
-    a = rng.integers(0, args.vocab_size, (63, 200))
-    b = rng.integers(0, args.vocab_size, (63, 40))
+    a = rng.integers(0, args.vocab_size, (B, 200))
+    b = rng.integers(0, args.vocab_size, (B, 40))
     outs = []
     for parts in (1, 2, 3, 4):
         ctx.set_batch_split(parts, min_tokens=1)
