@@ -264,6 +264,19 @@ def main():
     elapsed_serial = timed_steps(a.steps)
     stats = ctx.kernel_stats()
     ctx.kernel_timing(False)
+    ctx.set_batch_split(a.split if a.split is not None else 2)
+
+    # the same forward with the logits copied back to host memory every step
+    # (PCIe-inclusive; reported beside `value`, never as it)
+    host_logits = np.empty((B_PER_GPU, VS), np.float32)
+    d2h_steps = max(1, min(a.steps, 10))
+    dist.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(d2h_steps):
+        ctx.forward_dev(ids_dev, B_PER_GPU, SEQ, 0, logits_dev)
+        ctx.d2h(host_logits, logits_dev)
+    elapsed_d2h = dist.max(time.perf_counter() - t0)
 
     # sanity on the output (outside the timed region)
     probe = np.empty((2, VS), np.float32)
@@ -293,6 +306,7 @@ def main():
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "ms_per_step_serialized": round(elapsed_serial / a.steps * 1e3, 4),
         "batch_split": a.split if a.split is not None else 2,
+        "ms_per_step_with_logits_d2h": round(elapsed_d2h / d2h_steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
