@@ -195,6 +195,16 @@ int main(int argc, char** argv) {
     const int iters = argc > 2 ? atoi(argv[2]) : 10;
     const int M = 65536;
     const bool c5 = argc > 3 && std::string(argv[3]) == "c5";
+    if (argc > 3 && std::string(argv[3]) == "qkvepi") {  // what the QKV epilogue costs
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(4, 1, 4, 6, EPI_QKV, 3, 16),
+                   GVAR(4, 1, 4, 6, EPI_QKV, 2, 16), GVAR(2, 2, 4, 6, EPI_QKV, 2, 16)}, rounds, iters);
+        run_shape("QKV shape, plain store", EPI_STORE, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_STORE, 4, 16), GVAR(4, 1, 4, 6, EPI_STORE, 3, 16)}, rounds, iters);
+        run_shape("gate|up shape, plain store", EPI_STORE, M, 288, 1536, true,
+                  {GVAR(2, 2, 4, 4, EPI_STORE, 3, 16)}, rounds, iters);
+        return 0;
+    }
     if (!c5) {
     run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
               {RVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
