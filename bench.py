@@ -10,9 +10,13 @@ owns its 256 batch rows (weak scaling, reference rows are independent:
 llama3.py:163-211) and the step ends with the single RCCL gather of every rank's
 logits to rank 0 over xGMI.  Rank 0 prints one JSON line.
 
+value: the product forward (layers as two batch-row ranges on two HIP streams,
+l3_set_batch_split), no events in the timed region.
 roofline: the dominant kernel is the fused gate|up GEMM (N = 2*FD = 1536, K = 288,
 M = 65,536 rows) — algorithmic FLOPs 2*M*K*N per launch over its mean HIP-event
-duration on the context stream, against the 157.3 TFLOP/s dense fp32 MFMA peak.
+duration on the context stream, against the 157.3 TFLOP/s dense fp32 MFMA peak, timed in
+a second region of the same K steps with the split off (two row ranges in flight share
+the CUs, so a launch's duration would not measure the kernel): ms_per_step_serialized.
 "ffn" adds the down GEMM (the metric's "% fp32 MFMA peak on FFN GEMM").
 traffic: HBM bytes per gate|up launch from the committed rocprofv3 PMC summary
 (profiles/pmc_gateup.json, FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or null.
