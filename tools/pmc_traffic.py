@@ -44,7 +44,7 @@ def main():
     gu = [k for k in kernels if re.search(r"gemm_\w+_kernel<\d+, \d+, \d+, \d+, 2[,>]", k)]
     algo = 4 * (ROWS * D + 2 * FD * D + ROWS * FD)
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
-                     "python bench.py --steps 2 --warmup 1",
+                     "python bench.py --steps 2 --warmup 1 --split 1 (every launch full size)",
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
            "workload_rows": ROWS,
            "lib_version": sys.argv[4] if len(sys.argv) > 4 else None,
