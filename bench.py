@@ -1,7 +1,8 @@
 """Benchmark: stories15M batched prefill on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--global-batch G]
     (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+    --global-batch G: strong scaling instead (G rows split over the N GPUs; C4 is G = 2048)
 
 One step = one full forward (Llama.__call__ semantics: embedding, 6 blocks, final
 norm + lm_head on the last position) of B=256 sequences x L=256 tokens per GPU,
@@ -109,13 +110,13 @@ def cpu_baseline():
                       f"({t:.2f} s each), OpenBLAS threads={cores}"}
 
 
-def traffic_per_launch():
+def traffic_per_launch(rows):
     p = os.path.join(REPO, "profiles", "pmc_gateup.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
         d = json.load(f)
-    if d.get("workload_rows") != B_PER_GPU * SEQ or d.get("lib_version") != l3hip.version():
+    if d.get("workload_rows") != rows or d.get("lib_version") != l3hip.version():
         return None  # counters were measured on another build of the kernel
     return d.get("hbm_bytes_per_launch")
 
@@ -205,6 +206,8 @@ def main():
     ap.add_argument("--workload", choices=["c3", "c5"], default="c3",
                     help="c3: headline stories15M B=256 L=256 (default); c5: Llama-3-shape report")
     ap.add_argument("--layers", type=int, default=32, help="c5 only")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: this many rows split over the GPUs (default: 256 per GPU)")
     ap.add_argument("--split", type=int, default=None,
                     help="batch-split parts of the timed forward (default: the library's, 2)")
     a = ap.parse_args()
@@ -212,8 +215,16 @@ def main():
         return bench_c5(a)
 
     dist = Dist(a.gpus)
+    # default: weak scaling, B = 256 rows per GPU (N = 8 is C4's B = 2048); --global-batch G:
+    # strong scaling, G rows split over the N GPUs (C4 at any N)
+    if a.global_batch:
+        if a.global_batch % dist.world:
+            raise SystemExit(f"--global-batch {a.global_batch} not divisible by {dist.world} GPUs")
+        bpg = a.global_batch // dist.world
+    else:
+        bpg = B_PER_GPU
     dev = dist.local_rank
-    args = synth.stories15m(B_PER_GPU)
+    args = synth.stories15m(bpg)
     FD, D = synth.STORIES15M_HIDDEN, args.dim
     weights = synth.make_weights(args, FD, seed=0)
     with tempfile.TemporaryDirectory() as tmp:
@@ -224,18 +235,18 @@ def main():
     VS = args.vocab_size
 
     # inputs resident in HBM before the timed region
-    ids = np.random.default_rng(100 + dist.rank).integers(0, VS, (B_PER_GPU, SEQ)).astype(np.int32)
+    ids = np.random.default_rng(100 + dist.rank).integers(0, VS, (bpg, SEQ)).astype(np.int32)
     ids_dev = ctx.alloc(ids.nbytes)
     ctx.h2d(ids_dev, ids)
-    logits_dev = ctx.alloc(B_PER_GPU * VS * 4)
+    logits_dev = ctx.alloc(bpg * VS * 4)
     gathered_dev = None
-    rows = [B_PER_GPU] * dist.world
+    rows = [bpg] * dist.world
     dist.init_comm(ctx)
     if dist.world > 1 and dist.rank == 0:
-        gathered_dev = ctx.alloc(B_PER_GPU * dist.world * VS * 4)
+        gathered_dev = ctx.alloc(bpg * dist.world * VS * 4)
 
     def step():
-        ctx.forward_dev(ids_dev, B_PER_GPU, SEQ, 0, logits_dev)
+        ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
         if dist.world > 1:
             ctx.gather_logits(logits_dev, gathered_dev, rows, root=0)
 
@@ -272,13 +283,13 @@ def main():
 
     # the same forward with the logits copied back to host memory every step
     # (PCIe-inclusive; reported beside `value`, never as it)
-    host_logits = np.empty((B_PER_GPU, VS), np.float32)
+    host_logits = np.empty((bpg, VS), np.float32)
     d2h_steps = max(1, min(a.steps, 10))
     dist.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
     for _ in range(d2h_steps):
-        ctx.forward_dev(ids_dev, B_PER_GPU, SEQ, 0, logits_dev)
+        ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
         ctx.d2h(host_logits, logits_dev)
     elapsed_d2h = dist.max(time.perf_counter() - t0)
 
@@ -290,8 +301,8 @@ def main():
 
     if dist.rank != 0:
         return
-    tokens = B_PER_GPU * SEQ * dist.world * a.steps
-    T = B_PER_GPU * SEQ
+    tokens = bpg * SEQ * dist.world * a.steps
+    T = bpg * SEQ
     gu_ms, gu_n = stats["gateup"]
     dn_ms, dn_n = stats["down"]
     gu_flops = 2.0 * T * D * 2 * FD
@@ -299,7 +310,7 @@ def main():
     gu_avg_s = gu_ms / gu_n / 1e3
     achieved = gu_flops / gu_avg_s / 1e12
     ffn_tf = (gu_flops + dn_flops) / ((gu_ms / gu_n + dn_ms / dn_n) / 1e3) / 1e12
-    traffic = traffic_per_launch()
+    traffic = traffic_per_launch(T)
     out = {
         "metric": METRIC,
         "value": round(tokens / elapsed, 1),
@@ -312,14 +323,14 @@ def main():
         "batch_split": a.split if a.split is not None else 2,
         "ms_per_step_with_logits_d2h": round(elapsed_d2h / d2h_steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if a.global_batch else "weak",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic: stories15M-shaped N(0,0.02^2) weights (seed 0), uniform random ids",
-        "config": {"workload": f"stories15M prefill, B={B_PER_GPU} per GPU x L={SEQ}, start_pos 0",
-                   "global_batch": B_PER_GPU * dist.world, "seq_len": SEQ,
+        "config": {"workload": f"stories15M prefill, B={bpg} per GPU x L={SEQ}, start_pos 0",
+                   "global_batch": bpg * dist.world, "seq_len": SEQ,
                    "parallelism": f"dp{dist.world} (batch rows) + RCCL logits gather"},
-        "roofline": {"kernel": "gemm gate|up (fused SwiGLU epilogue), M=65536 K=288 N=1536",
+        "roofline": {"kernel": f"gemm gate|up (fused SwiGLU epilogue), M={T} K=288 N=1536",
                      "pass": "same workload and step count, batch split off (HIP events need "
                              "the kernel alone on the CUs)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
