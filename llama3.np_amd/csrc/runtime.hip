@@ -32,6 +32,8 @@
 
 using namespace l3;
 
+static_assert(offsetof(DecState, pos) == 0, "captured kernels read &DecState::pos as pos_dev");
+
 static thread_local std::string g_err;
 
 static int fail(const char* fmt, ...) {
