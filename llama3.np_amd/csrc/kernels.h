@@ -46,7 +46,6 @@ struct DecState {
     int32_t* hist;     // null: no history
 };
 
-
 // row r of A (identity, or the gathered embedding row)
 __device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
     return p.A + (p.a_rows ? (int64_t)p.a_rows[r] : r) * p.lda;
