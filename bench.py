@@ -103,7 +103,19 @@ def cpu_baseline():
         model(ids, 0)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
+    # SURVEY 8(d) / BASELINE.md: a 1-thread figure beside the all-cores one (B = 4 sample)
+    one = None
+    try:
+        from threadpoolctl import threadpool_limits
+
+        with threadpool_limits(limits=1):
+            t1 = time.perf_counter()
+            model(ids[:4], 0)
+            one = round(4 * SEQ / (time.perf_counter() - t1), 1)
+    except Exception:
+        pass
     return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(cores),
+            "value_1_thread": one,
             "kind": "port",
             "sample": f"oracle/llama3_oracle.py (NumPy restatement of the reference, f64 after layer-0 "
                       f"RoPE as the reference) stories15M prefill B={Bs} L={SEQ}, median of 2 "
