@@ -207,6 +207,37 @@ def bench_c5(a):
         "kernels": per, "weight_upload_s": round(t_up, 1)}))
 
 
+def cpu_c5_slice():
+    """BASELINE.md / SURVEY 8(d): the reference's CPU path on C5 is infeasible in full, so the
+    oracle (NumPy restatement, f64 after layer-0 RoPE) is timed on a 2-layer Llama-3-shape slice
+    at B = 1, L = 2048 on this host and extrapolated x16 layers x64 sequences (labelled so)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import llama3_oracle as orc
+
+    args = synth.llama3_shape(n_layers=2, max_batch_size=1, max_seq_len=2048)
+    t_gen = time.perf_counter()
+    w = synth.make_weights(args, synth.LLAMA3_HIDDEN, seed=0)
+    t_gen = time.perf_counter() - t_gen
+    model = orc.OracleModel(w, args)
+    ids = np.random.default_rng(1).integers(0, args.vocab_size, (1, 2048))
+    t0 = time.perf_counter()
+    out = model(ids, 0)
+    t = time.perf_counter() - t0
+    assert np.isfinite(out).all()
+    full_s = t * (32 / 2) * 64
+    try:
+        from threadpoolctl import threadpool_info
+
+        cores = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    print(json.dumps({
+        "metric": "CPU baseline, Llama-3-shape prefill B=64 L=2048 (BASELINE configs[4]), extrapolated",
+        "slice": "oracle, 2 of 32 layers, B=1, L=2048, one forward", "slice_s": round(t, 2),
+        "extrapolated_full_s": round(full_s, 0), "value": round(64 * 2048 / full_s, 2),
+        "unit": "tokens/s", "kind": "port", "cores": int(cores), "weight_gen_s": round(t_gen, 1)}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,8 +246,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-breakdown", action="store_true",
                     help="skip the untimed all-kernel event pass (profiling runs)")
-    ap.add_argument("--workload", choices=["c3", "c5"], default="c3",
-                    help="c3: headline stories15M B=256 L=256 (default); c5: Llama-3-shape report")
+    ap.add_argument("--workload", choices=["c3", "c5", "c5cpu"], default="c3",
+                    help="c3: headline stories15M B=256 L=256 (default); c5: Llama-3-shape report; "
+                         "c5cpu: the oracle on a 2-layer C5 slice, extrapolated")
     ap.add_argument("--layers", type=int, default=32, help="c5 only")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="strong scaling: this many rows split over the GPUs (default: 256 per GPU)")
@@ -225,6 +257,8 @@ def main():
     a = ap.parse_args()
     if a.workload == "c5":
         return bench_c5(a)
+    if a.workload == "c5cpu":
+        return cpu_c5_slice()
 
     dist = Dist(a.gpus)
     # default: weak scaling, B = 256 rows per GPU (N = 8 is C4's B = 2048); --global-batch G:
