@@ -283,6 +283,22 @@ def test_batch_split_bit_identical(tmpdir_mod, B):
     ctx.set_batch_split(2)
 
 
+def test_sharded_prefill_world1_rccl(tmpdir_mod):
+    """ShardedPrefill.on_device at world 1: the RCCL communicator, the logits gather to the
+    root and the D2H, against Llama.__call__ on the same rows (bit-identical: same kernels)."""
+    from sharded import ShardedPrefill
+
+    args = synth.stories15m(4)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    ids = np.random.default_rng(31).integers(0, args.vocab_size, (4, 33))
+    want = llama3.Llama(path, args)(ids, 0)
+    m = llama3.Llama(path, args)
+    sp = ShardedPrefill.on_device(m, 1, 0, bcast_uid=lambda uid: uid)
+    got = sp(ids, 0)
+    assert got.shape == want.shape
+    np.testing.assert_array_equal(got, want)
+
+
 # ---- decode state / graph replay ------------------------------------------------------------
 
 @pytest.mark.parametrize("case", ["all_equal", "pair_tie_zero_rest", "nan_rows"])
