@@ -389,6 +389,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline()
     if dist.world == 1 and not a.no_kernel_breakdown:
         # per-kernel breakdown from a separate (untimed, serialized) pass with all events on
+        ctx.set_batch_split(1)
         ctx.kernel_timing(True)
         for _ in range(3):
             step()

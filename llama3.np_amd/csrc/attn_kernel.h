@@ -166,8 +166,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                         sacc[kg][r] = v;
                         mt = fmaxf(mt, v);
                     }
-                mt = fmaxf(mt, __shfl_xor(mt, 16));
-                mt = fmaxf(mt, __shfl_xor(mt, 32));
+                mt = max_xor16_32(mt);
                 const float m_new = fmaxf(m_run[j], mt);
                 // v_exp_f32 directly: arguments are <= 0 (exact 0 at -inf), so the libm
                 // denormal-range guard around exp2f is dead weight (5 VALU per call)
@@ -218,8 +217,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
     for (int j = 0; j < QBW; ++j) {
         float l = l_run[j];
-        l += __shfl_xor(l, 16);
-        l += __shfl_xor(l, 32);
+        l = sum_xor16_32(l);
         const int ql = q_lo + qblk[j] * 16 + fq;
         if (ql < p.L) {
             const float inv = 1.0f / l;

@@ -411,8 +411,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         float v = ss[i];
-        v += __shfl_xor(v, 16);  // the four k-quarters of the row
-        v += __shfl_xor(v, 32);
+        v = sum_xor16_32(v);  // the four k-quarters of the row
         rs[i] = p.norm ? 1.0f / sqrtf(v * inv_k + p.eps) : 1.0f;
     }
     L3_STAMP(2);

@@ -46,6 +46,23 @@ struct DecState {
     int32_t* hist;     // null: no history
 };
 
+// Exchange with lane ^ 16 and lane ^ 32 through v_permlane16_swap / v_permlane32_swap (VALU)
+// rather than ds_bpermute: a bpermute is an LDS-pipe round trip whose lgkmcnt wait also
+// drains the wave's outstanding LDS fragment reads.  With both operands the same register,
+// lane i of the pair returned holds {v[i], v[i ^ 16]} (resp. ^ 32) in some order.
+__device__ __forceinline__ float max_xor16_32(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float sum_xor16_32(float v) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
+
 // row r of A (identity, or the gathered embedding row)
 __device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
     return p.A + (p.a_rows ? (int64_t)p.a_rows[r] : r) * p.lda;
