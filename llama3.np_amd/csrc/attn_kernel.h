@@ -276,8 +276,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
         sc[k] = s;
         m = fmaxf(m, s);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    m = group_max<64>(m);
     if (lane == 0) wred[wid] = m;
     __syncthreads();
     m = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
@@ -288,8 +287,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
         sc[k] = e;
         l += e;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) l += __shfl_xor(l, o);
+    l = group_sum<64>(l);
     if (lane == 0) wred[4 + wid] = l;
     __syncthreads();  // p complete in LDS; row sum in wred[4..7]
     l = (wred[4] + wred[5]) + (wred[6] + wred[7]);

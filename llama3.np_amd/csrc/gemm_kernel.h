@@ -555,14 +555,13 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             }
         }
     }
+    // the LPU lanes of a unit are one aligned group: VALU-only reduction (no LDS round trips)
 #pragma unroll
-    for (int o = LPU / 2; o > 0; o >>= 1)
+    for (int m = 0; m < MR; ++m) {
+        ss[m] = group_sum<LPU>(ss[m]);
 #pragma unroll
-        for (int m = 0; m < MR; ++m) {
-            ss[m] += __shfl_xor(ss[m], o);
-#pragma unroll
-            for (int r = 0; r < ROWS; ++r) acc[r][m] += __shfl_xor(acc[r][m], o);
-        }
+        for (int r = 0; r < ROWS; ++r) acc[r][m] = group_sum<LPU>(acc[r][m]);
+    }
     if (!writer) return;
 #pragma unroll
     for (int mi = 0; mi < MR; ++mi) {

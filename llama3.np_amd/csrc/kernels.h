@@ -63,6 +63,50 @@ __device__ __forceinline__ float sum_xor16_32(float v) {
     return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// Reductions over aligned groups of LANES = 16, 32 or 64 lanes, every lane of a group left
+// with its result, all on the VALU: DPP quad_perm (lane ^ 1, lane ^ 2), row_half_mirror and
+// row_mirror complete 16-lane rows (each step pairs lanes whose partial sums cover disjoint
+// halves), then the permlane swaps above.  Each step adds the same two values on both lanes of
+// a pair, so all lanes agree bit for bit.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int LANES>
+__device__ __forceinline__ float group_sum(float v) {
+    static_assert(LANES == 16 || LANES == 32 || LANES == 64, "16, 32 or 64 lanes");
+    v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);  // row_half_mirror
+    v += dpp_mov<0x140>(v);  // row_mirror
+    if constexpr (LANES >= 32) {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    }
+    if constexpr (LANES >= 64) {
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+    }
+    return v;
+}
+template <int LANES>
+__device__ __forceinline__ float group_max(float v) {
+    static_assert(LANES == 16 || LANES == 32 || LANES == 64, "16, 32 or 64 lanes");
+    v = fmaxf(v, dpp_mov<0xB1>(v));
+    v = fmaxf(v, dpp_mov<0x4E>(v));
+    v = fmaxf(v, dpp_mov<0x141>(v));
+    v = fmaxf(v, dpp_mov<0x140>(v));
+    if constexpr (LANES >= 32) {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+    }
+    if constexpr (LANES >= 64) {
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+        v = fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+    }
+    return v;
+}
+
 // row r of A (identity, or the gathered embedding row)
 __device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
     return p.A + (p.a_rows ? (int64_t)p.a_rows[r] : r) * p.lda;
