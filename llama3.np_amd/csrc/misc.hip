@@ -29,6 +29,36 @@ __device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi) 
     return v > bv || (v == bv && i < bi);
 }
 
+// (value, index) argmax over aligned groups of LANES lanes on the VALU (the group_sum pattern of
+// kernels.h: DPP quad_perm / row mirrors, then permlane swaps); argmax_better is a strict total
+// order, so the winner does not depend on the pairing
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int LANES>
+__device__ __forceinline__ void group_argmax(float& best, int& bi, int lane) {
+    auto step = [&](float ov, int oi) {
+        if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+    };
+    step(__int_as_float(dpp_mov_i<0xB1>(__float_as_int(best))), dpp_mov_i<0xB1>(bi));
+    step(__int_as_float(dpp_mov_i<0x4E>(__float_as_int(best))), dpp_mov_i<0x4E>(bi));
+    step(__int_as_float(dpp_mov_i<0x141>(__float_as_int(best))), dpp_mov_i<0x141>(bi));
+    step(__int_as_float(dpp_mov_i<0x140>(__float_as_int(best))), dpp_mov_i<0x140>(bi));
+    if constexpr (LANES >= 32) {  // lane i of the swapped pair: {own, lane ^ 16}, partner second in rows 0, 2
+        const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+        const auto x = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
+        const bool hi = lane & 16;
+        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
+    }
+    if constexpr (LANES >= 64) {
+        const auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+        const auto x = __builtin_amdgcn_permlane32_swap((unsigned)bi, (unsigned)bi, false, false);
+        const bool hi = lane & 32;
+        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
+    }
+}
+
 __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ x, int n,
                                                       int32_t* __restrict__ out,
                                                       DecState* __restrict__ st) {
@@ -59,12 +89,7 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
         for (int i = tid; i < n; i += NT)
             if (argmax_better(row[i], i, best, bi)) { best = row[i]; bi = i; }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(best, o);
-        const int oi = __shfl_xor(bi, o);
-        if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
-    }
+    group_argmax<64>(best, bi, tid & 63);
     __shared__ float sv[NT / 64];
     __shared__ int si[NT / 64];
     if ((tid & 63) == 0) { sv[tid >> 6] = best; si[tid >> 6] = bi; }
@@ -72,12 +97,7 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
     if (tid < 64) {
         best = tid < NT / 64 ? sv[tid] : -INFINITY;
         bi = tid < NT / 64 ? si[tid] : 0x7fffffff;
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) {
-            const float ov = __shfl_xor(best, o);
-            const int oi = __shfl_xor(bi, o);
-            if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
-        }
+        group_argmax<16>(best, bi, tid);  // the NT / 64 = 16 wave results in lanes 0-15
         if (tid == 0) {
             out[blockIdx.x] = bi;
             if (st) {
