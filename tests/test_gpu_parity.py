@@ -299,6 +299,38 @@ def test_sharded_prefill_world1_rccl(tmpdir_mod):
     np.testing.assert_array_equal(got, want)
 
 
+def test_gather_overlaps_next_forward_world1(tmpdir_mod):
+    """The logits gather runs on the comm stream: step k's gather overlaps step k+1's layers
+    and step k+1's lm_head waits for it (one logits buffer reused, as bench.py does).  Three
+    pipelined forwards, two gathers into separate roots, then D2H: each holds its own step's
+    logits, bit-identical to Llama.__call__ on the same rows, under each batch split."""
+    args = synth.stories15m(16)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    VS, B, L = args.vocab_size, 16, 64
+    rng = np.random.default_rng(41)
+    ids = [rng.integers(0, VS, (B, L)).astype(np.int32) for _ in range(3)]
+    ref = llama3.Llama(path, args)
+    want = [ref(x, 0)[:, 0, :] for x in ids]
+    m = llama3.Llama(path, args)
+    ctx = m.context
+    ctx.comm_init(1, 0, l3hip.comm_unique_id())
+    ids_dev = [ctx.alloc(x.nbytes) for x in ids]
+    for d, x in zip(ids_dev, ids):
+        ctx.h2d(d, x)
+    buf = ctx.alloc(B * VS * 4)
+    dst = [ctx.alloc(B * VS * 4) for _ in range(2)]
+    for parts in (1, 2):
+        ctx.set_batch_split(parts, min_tokens=1)
+        for k in range(3):
+            ctx.forward_dev(ids_dev[k], B, L, 0, buf)
+            if k < 2:
+                ctx.gather_logits(buf, dst[k], [B], root=0)
+        got = [ctx.d2h(np.empty((B, VS), np.float32), p) for p in (dst[0], dst[1], buf)]
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(g, w)
+    ctx.set_batch_split(2)
+
+
 # ---- decode state / graph replay ------------------------------------------------------------
 
 @pytest.mark.parametrize("case", ["all_equal", "pair_tie_zero_rest", "nan_rows"])
