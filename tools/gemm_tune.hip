@@ -195,6 +195,15 @@ int main(int argc, char** argv) {
     const int iters = argc > 2 ? atoi(argv[2]) : 10;
     const int M = 65536;
     const bool c5 = argc > 3 && std::string(argv[3]) == "c5";
+    if (argc > 3 && std::string(argv[3]) == "qkvq") {  // QKV tiles by whole block rounds
+        // 128x96: 4608 blocks = 4.5 rounds at 4 blocks/CU; 128x144: 3072 = 3 (4/CU) or 4 (3/CU);
+        // 64x96: 9216 = 9 rounds at 4/CU
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(4, 1, 2, 9, EPI_QKV, 3, 16),
+                   GVAR(4, 1, 2, 9, EPI_QKV, 4, 16), GVAR(2, 2, 2, 3, EPI_QKV, 4, 16),
+                   GVAR(2, 2, 2, 3, EPI_QKV, 5, 16), GVAR(4, 1, 2, 9, EPI_QKV, 3, 32)}, rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "qkvepi") {  // what the QKV epilogue costs
         run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
                   {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(4, 1, 4, 6, EPI_QKV, 3, 16),
