@@ -204,6 +204,18 @@ int main(int argc, char** argv) {
                    GVAR(2, 2, 2, 3, EPI_QKV, 5, 16), GVAR(4, 1, 2, 9, EPI_QKV, 3, 32)}, rounds, iters);
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "resq") {  // O-proj / down tiles by block rounds
+        // N = 288: 128x144 (4x1 waves of 32x144) = 1024 blocks, one round at 4 blocks/CU
+        run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
+                  {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), GVAR(4, 1, 2, 9, EPI_RESID, 4, 16),
+                   GVAR(4, 1, 2, 9, EPI_RESID, 3, 16), GVAR(2, 2, 2, 3, EPI_RESID, 4, 16),
+                   GVAR(4, 1, 1, 9, EPI_RESID, 4, 16)}, rounds, iters);
+        run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
+                  {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(4, 1, 2, 9, EPI_RESID, 4, 16),
+                   GVAR(4, 1, 2, 9, EPI_RESID, 3, 16), GVAR(4, 1, 2, 9, EPI_RESID, 2, 32),
+                   GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "qkvepi") {  // what the QKV epilogue costs
         run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
                   {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(4, 1, 4, 6, EPI_QKV, 3, 16),
