@@ -97,7 +97,8 @@ static void run(const char* label, int B, int L, int H, int KVH, int HD, std::ve
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
     run("stories15M C3", 256, 256, 6, 6, 48,
-        {AVAR(48, 4, 1, 64), AVAR(48, 4, 1, 32), AVAR(48, 2, 1, 64)}, rounds, iters);
+        {AVAR(48, 4, 1, 64), AVAR(48, 4, 1, 32), AVAR(48, 2, 1, 64), AVAR(48, 2, 1, 32),
+         AVAR(48, 1, 1, 32), AVAR(48, 1, 1, 64)}, rounds, iters);
     run("Llama-3 shape (C5 slice)", 4, 2048, 32, 8, 128,
         {AVAR(128, 1, 4, 32), AVAR(128, 2, 4, 32)}, rounds, 3);
     return 0;
