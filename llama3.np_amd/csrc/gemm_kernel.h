@@ -343,12 +343,27 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         // (__syncthreads would drain every outstanding glds).  Per iteration: wait until tile
         // kt has landed (this wave's pieces), barrier (everyone's pieces landed, everyone done
         // with tile kt - 1), refill the slot of tile kt - 1 with tile kt + NS - 1, compute.
-        constexpr int G = (BM / RP + 3) / 4 + (BN / RP + 3) / 4;  // glds per wave per tile
+        // glds per wave per tile: pieces go round-robin over the 4 waves, so when a tile's
+        // piece count is not a multiple of 4 the first (count % 4) waves issue one more; each
+        // wave's counted wait must use its own count (with the larger count for every wave, a
+        // wave issuing fewer would not wait for its own pieces of tile kt: stale LDS rows)
+        constexpr int AP = BM / RP, BP = BN / RP;
+        constexpr int GA_HI = (AP + 3) / 4, GA_LO = AP / 4, GB_HI = (BP + 3) / 4, GB_LO = BP / 4;
+        const bool a_hi = AP % 4 == 0 || wid < AP % 4, b_hi = BP % 4 == 0 || wid < BP % 4;
+        auto wait_ring = [&]() {  // wave-uniform branches over compile-time counts
+            if (a_hi) {
+                if (b_hi) wait_vmcnt<(NS - 2) * (GA_HI + GB_HI)>();
+                else wait_vmcnt<(NS - 2) * (GA_HI + GB_LO)>();
+            } else {
+                if (b_hi) wait_vmcnt<(NS - 2) * (GA_LO + GB_HI)>();
+                else wait_vmcnt<(NS - 2) * (GA_LO + GB_LO)>();
+            }
+        };
 #pragma unroll
         for (int i = 0; i < NS - 1; ++i)
             if (i < nk) glds_tile(i, i * BK);
         for (int kt = 0; kt < nk; ++kt) {
-            if (kt + NS - 2 < nk) wait_vmcnt<(NS - 2) * G>();
+            if (kt + NS - 2 < nk) wait_ring();
             else wait_vmcnt<0>();
             // this wave's LDS reads of tile kt - 1 are done before anyone refills its slot
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
