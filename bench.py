@@ -9,7 +9,9 @@ norm + lm_head on the last position) of B=256 sequences x L=256 tokens per GPU,
 start_pos 0, ids already resident in HBM, logits left in HBM; for N > 1 each rank
 owns its 256 batch rows (weak scaling, reference rows are independent:
 llama3.py:163-211) and the step ends with the single RCCL gather of every rank's
-logits to rank 0 over xGMI.  Rank 0 prints one JSON line.
+logits to rank 0 over xGMI (on the library's comm stream: step k's gather overlaps
+step k+1's layers; the timed region's closing synchronize waits for the last one).
+Rank 0 prints one JSON line.
 
 value: the product forward (layers as two batch-row ranges on two HIP streams,
 l3_set_batch_split), no events in the timed region.

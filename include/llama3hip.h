@@ -179,7 +179,11 @@ int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
 int l3_comm_unique_id(uint8_t id_out[128]);
 int l3_comm_init(l3_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 /* Gather each rank's logits rows [rows_r, VS] (device) into root's dst_dev
- * [sum rows, VS] in rank order; rows_per_rank has nranks entries.  Async. */
+ * [sum rows, VS] in rank order; rows_per_rank has nranks entries.  Async, on
+ * the context's comm stream after the work queued so far: the next
+ * l3_forward_dev overlaps it with its layers and waits for it only before its
+ * lm_head (the writer of src); every other call (l3_d2h of dst_dev,
+ * l3_synchronize, ...) waits for it first. */
 int l3_comm_gather_logits(l3_ctx* ctx, const float* src_dev, float* dst_dev,
                           const int64_t* rows_per_rank, int32_t root);
 int l3_comm_barrier(l3_ctx* ctx);

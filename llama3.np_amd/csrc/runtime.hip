@@ -119,6 +119,12 @@ struct l3_ctx {
     // rccl
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // the logits gather runs on its own stream, so step k's transfer over xGMI overlaps step
+    // k+1's layers; the next lm_head (the writer of the gathered rows) waits for it, every
+    // other entry point joins it first (set_dev)
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t comm_fwd_ev = nullptr, comm_done_ev = nullptr;
+    bool gather_pending = false;
     // captured greedy decode step (llama3.py:316-320 as one hipGraph replay per token)
     int32_t* dec_ids = nullptr;      // [maxB] input ids of the next decode step (argmax output)
     DecState* dec_state = nullptr;   // device loop state: position, generate history
@@ -133,8 +139,14 @@ struct l3_ctx {
 };
 
 // ---------------------------------------------------------------------------------------
-static int set_dev(l3_ctx* c) {
+// join = the context stream waits for an in-flight logits gather: every entry point except
+// l3_forward_dev (which waits only before its lm_head) and the gather itself
+static int set_dev(l3_ctx* c, bool join = true) {
     HIP_TRY(hipSetDevice(c->device));
+    if (join && c->gather_pending) {
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->comm_done_ev, 0));
+        c->gather_pending = false;
+    }
     return 0;
 }
 
@@ -300,7 +312,11 @@ extern "C" int l3_destroy(l3_ctx* c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+    if (c->comm_fwd_ev) (void)hipEventDestroy(c->comm_fwd_ev);
+    if (c->comm_done_ev) (void)hipEventDestroy(c->comm_done_ev);
     for (auto& L : c->layers) {
         dfree(L.wqkv); dfree(L.wo); dfree(L.wgu); dfree(L.wd); dfree(L.n_attn); dfree(L.n_ffn);
         dfree(L.cache_k); dfree(L.cache_v);
@@ -595,6 +611,12 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
             rc = run_layer(c, li, nb[p], L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr, b0[p], st[p]);
         roctxRangePop();
     }
+    // the previous step's gather may still read the logits rows: the lm_head streams wait for
+    // it (stream joins the parts below, so it has waited too once the forward returns)
+    if (c->gather_pending && !rc) {
+        for (int p = 0; p < (lm_parts ? parts : 1); ++p) HIP_TRY(hipStreamWaitEvent(st[p], c->comm_done_ev, 0));
+        c->gather_pending = false;
+    }
     roctxRangePushA("l3.lm_head");
     for (int p = 0; p < parts && lm_parts && !rc; ++p) rc = run_lm_head(c, nb[p], L, logits_dev, b0[p], st[p]);
     roctxRangePop();
@@ -637,7 +659,8 @@ extern "C" int l3_set_batch_split(l3_ctx* c, int32_t parts, int64_t min_tokens) 
 extern "C" int l3_forward_dev(l3_ctx* c, const int32_t* ids_dev, int32_t B, int32_t L,
                               int32_t start_pos, float* logits_dev) {
     CHECK_CTX(c);
-    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
+    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c, false) || ensure_ws(c, B, L))
+        return 1;
     return forward_dev(c, ids_dev, B, L, start_pos, logits_dev);
 }
 
@@ -1064,6 +1087,11 @@ extern "C" int l3_comm_unique_id(uint8_t id_out[128]) {
 extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
     CHECK_CTX(c);
     if (set_dev(c)) return 1;
+    if (!c->comm_stream) {
+        HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&c->comm_fwd_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&c->comm_done_ev, hipEventDisableTiming));
+    }
     ncclUniqueId uid;
     memcpy(&uid, id, 128);
     NCCL_TRY(ncclCommInitRank(&c->comm, nranks, uid, rank));
@@ -1076,8 +1104,13 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
                                      const int64_t* rows_per_rank, int32_t root) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_gather_logits: communicator not initialised");
-    if (set_dev(c)) return 1;
+    if (set_dev(c, false)) return 1;
     const int64_t VS = c->d.vocab_size;
+    // on comm_stream after everything queued so far on stream (the forward that wrote src);
+    // a previous gather is ordered before it by comm_stream itself
+    HIP_TRY(hipEventRecord(c->comm_fwd_ev, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->comm_fwd_ev, 0));
+    hipStream_t s = c->comm_stream;
     // RCCL has no native gather: root posts one recv per peer, peers one send, all in one
     // group so the point-to-point transfers run concurrently over the xGMI links.
     NCCL_TRY(ncclGroupStart());
@@ -1088,22 +1121,23 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
             if (r == root) {
                 if (n && dst_dev + off * VS != src_dev) {
                     const hipError_t e = hipMemcpyAsync(dst_dev + off * VS, src_dev, n * 4,
-                                                        hipMemcpyDeviceToDevice, c->stream);
+                                                        hipMemcpyDeviceToDevice, s);
                     if (e != hipSuccess) {
                         (void)ncclGroupEnd();  // close the group before reporting
                         return fail("gather root copy: %s", hipGetErrorString(e));
                     }
                 }
             } else if (n) {
-                NCCL_TRY(ncclRecv(dst_dev + off * VS, (size_t)n, ncclFloat32, r, c->comm, c->stream));
+                NCCL_TRY(ncclRecv(dst_dev + off * VS, (size_t)n, ncclFloat32, r, c->comm, s));
             }
             off += rows_per_rank[r];
         }
     } else if (rows_per_rank[c->rank]) {
-        NCCL_TRY(ncclSend(src_dev, (size_t)(rows_per_rank[c->rank] * VS), ncclFloat32, root, c->comm,
-                          c->stream));
+        NCCL_TRY(ncclSend(src_dev, (size_t)(rows_per_rank[c->rank] * VS), ncclFloat32, root, c->comm, s));
     }
     NCCL_TRY(ncclGroupEnd());
+    HIP_TRY(hipEventRecord(c->comm_done_ev, s));
+    c->gather_pending = true;
     return 0;
 }
 

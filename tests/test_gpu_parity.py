@@ -300,10 +300,11 @@ def test_sharded_prefill_world1_rccl(tmpdir_mod):
 
 
 def test_gather_pipelined_forwards_world1(tmpdir_mod):
-    """Forwards and gathers queued back to back on one logits buffer, as bench.py does (the
-    gather is ordered on the context stream): three forwards, two gathers into separate roots,
-    then D2H — each holds its own step's logits, bit-identical to Llama.__call__ on the same
-    rows, under each batch split."""
+    """Forwards and gathers queued back to back on one logits buffer, as bench.py does: the
+    gather runs on the comm stream, overlapping the next forward's layers, and the next
+    lm_head waits for it.  Three forwards, two gathers into separate roots, then D2H — each
+    holds its own step's logits, bit-identical to Llama.__call__ on the same rows, under each
+    batch split."""
     args = synth.stories15m(16)
     _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
     VS, B, L = args.vocab_size, 16, 64
@@ -328,8 +329,8 @@ def test_gather_pipelined_forwards_world1(tmpdir_mod):
         got = [ctx.d2h(np.empty((B, VS), np.float32), p) for p in (dst[0], dst[1], buf)]
         for g, w in zip(got, want):
             np.testing.assert_array_equal(g, w)
-    # a gather queued before a different entry point runs (a greedy step here): the gathered
-    # rows stay those of their own step
+    # a gather still in flight when a different entry point runs (a greedy step here): that
+    # call joins the comm stream first, and the gathered rows stay those of their own step
     ctx.forward_dev(ids_dev[0], B, L, 0, buf)
     ctx.gather_logits(buf, dst[0], [B], root=0)
     nxt, _ = ctx.greedy_step(ids[1], 0)

@@ -1,8 +1,8 @@
 """Diagnostic: repeat the pipelined forward / gather sequence of
 tests/test_gpu_parity.py::test_gather_pipelined_forwards_world1 and report every
 mismatch (which buffer, which rows / columns, and whose logits the wrong values are).
-Also runs the same forwards with no gather at all (control).  The gather is ordered on the
-context stream; this replays the sequence that once failed with an overlapped-gather build."""
+Also runs the same forwards with no gather at all (control).  Usage:
+    python tools/gather_race_check.py [reps] [B] [L]"""
 import os
 import sys
 import tempfile
@@ -16,12 +16,14 @@ import llama3  # noqa: E402
 import synth  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-args = synth.stories15m(16)
+B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+L = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+args = synth.stories15m(B)
 w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=0)
 tmp = tempfile.mkdtemp()
 path = os.path.join(tmp, "m.npz")
 synth.save_npz(path, w)
-VS, B, L = args.vocab_size, 16, 64
+VS = args.vocab_size
 rng = np.random.default_rng(41)
 ids = [rng.integers(0, VS, (B, L)).astype(np.int32) for _ in range(3)]
 ref = llama3.Llama(path, args)
