@@ -186,6 +186,13 @@ int l3_comm_init(l3_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128
  * l3_synchronize, ...) waits for it first. */
 int l3_comm_gather_logits(l3_ctx* ctx, const float* src_dev, float* dst_dev,
                           const int64_t* rows_per_rank, int32_t root);
+/* Greedy ids only (SURVEY 8(e) option): argmax of each rank's logits rows
+ * [rows_r, VS] (device; first index on ties, llama3.py:320) gathered as int32
+ * into root's ids_dst_dev [sum rows] in rank order — B x 4 bytes over xGMI
+ * instead of B x VS x 4.  Ordered on the context stream.  Replaces the host
+ * np.argmax of llama3.py:320 over the gathered logits. */
+int l3_comm_gather_argmax(l3_ctx* ctx, const float* logits_dev, int32_t* ids_dst_dev,
+                          const int64_t* rows_per_rank, int32_t root);
 int l3_comm_barrier(l3_ctx* ctx);
 /* max over ranks of one host double (in place; synchronous) — e.g. step time */
 int l3_comm_allreduce_max(l3_ctx* ctx, double* value);

@@ -123,6 +123,7 @@ struct l3_ctx {
     // k+1's layers; the next lm_head (the writer of the gathered rows) waits for it, every
     // other entry point joins it first (set_dev)
     hipStream_t comm_stream = nullptr;
+    int32_t* gather_ids = nullptr;   // [maxB] this rank's argmax ids (l3_comm_gather_argmax)
     hipEvent_t comm_fwd_ev = nullptr, comm_done_ev = nullptr;
     bool gather_pending = false;
     // captured greedy decode step (llama3.py:316-320 as one hipGraph replay per token)
@@ -323,7 +324,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     }
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
-    dfree(c->amax);
+    dfree(c->amax); dfree(c->gather_ids);
     for (void* p : c->scratch) dfree(p);
     for (auto& t : c->timers) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     drop_decode_graph(c);
@@ -1138,6 +1139,46 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
     NCCL_TRY(ncclGroupEnd());
     HIP_TRY(hipEventRecord(c->comm_done_ev, s));
     c->gather_pending = true;
+    return 0;
+}
+
+// SURVEY 8(e) option: greedy ids only — each rank's argmax over its [rows_r, VS] logits
+// (llama3.py:320: first index on ties, as the decode argmax) on the device, then the
+// B x 4-byte ids gathered to the root instead of the B x VS x 4-byte logits.
+extern "C" int l3_comm_gather_argmax(l3_ctx* c, const float* src_dev, int32_t* dst_dev,
+                                     const int64_t* rows_per_rank, int32_t root) {
+    CHECK_CTX(c);
+    if (!c->comm) return fail("l3_comm_gather_argmax: communicator not initialised");
+    if (set_dev(c)) return 1;
+    const int64_t n = rows_per_rank[c->rank], maxB = c->d.max_batch_size;
+    if (n < 0 || n > maxB)
+        return fail("l3_comm_gather_argmax: %lld rows on this rank, max_batch_size %lld",
+                    (long long)n, (long long)maxB);
+    if (!c->gather_ids) HIP_TRY(hipMalloc(&c->gather_ids, (maxB > 0 ? maxB : 1) * 4));
+    if (n) HIP_TRY(launch_argmax(src_dev, n, (int)c->d.vocab_size, c->gather_ids, c->stream));
+    NCCL_TRY(ncclGroupStart());
+    if (c->rank == root) {
+        int64_t off = 0;
+        for (int r = 0; r < c->nranks; ++r) {
+            const int64_t m = rows_per_rank[r];
+            if (r == root) {
+                if (m) {
+                    const hipError_t e = hipMemcpyAsync(dst_dev + off, c->gather_ids, m * 4,
+                                                        hipMemcpyDeviceToDevice, c->stream);
+                    if (e != hipSuccess) {
+                        (void)ncclGroupEnd();
+                        return fail("gather_argmax root copy: %s", hipGetErrorString(e));
+                    }
+                }
+            } else if (m) {
+                NCCL_TRY(ncclRecv(dst_dev + off, (size_t)m, ncclInt32, r, c->comm, c->stream));
+            }
+            off += m;
+        }
+    } else if (n) {
+        NCCL_TRY(ncclSend(c->gather_ids, (size_t)n, ncclInt32, root, c->comm, c->stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
     return 0;
 }
 

@@ -77,6 +77,7 @@ _SIGNATURES = {
     "l3_comm_unique_id": (ctypes.c_int, [_P]),
     "l3_comm_init": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "l3_comm_gather_logits": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
+    "l3_comm_gather_argmax": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
     "l3_comm_barrier": (ctypes.c_int, [_P]),
     "l3_comm_allreduce_max": (ctypes.c_int, [_P, _P]),
 }
@@ -255,6 +256,12 @@ class Context:
     def gather_logits(self, src_dev: int, dst_dev: Optional[int], rows_per_rank, root: int = 0):
         rows = np.ascontiguousarray(rows_per_rank, dtype=np.int64)
         check(lib().l3_comm_gather_logits(self._h, src_dev, dst_dev or 0, ptr(rows), root))
+
+    def gather_argmax(self, src_dev: int, dst_dev: Optional[int], rows_per_rank, root: int = 0):
+        """Greedy ids only: each rank's argmax over its logits rows, int32 ids gathered to
+        ``dst_dev`` [sum rows] on the root (SURVEY 8(e) option)."""
+        rows = np.ascontiguousarray(rows_per_rank, dtype=np.int64)
+        check(lib().l3_comm_gather_argmax(self._h, src_dev, dst_dev or 0, ptr(rows), root))
 
     def comm_barrier(self) -> None:
         check(lib().l3_comm_barrier(self._h))

@@ -38,13 +38,16 @@ class ShardedPrefill:
 
     forward_local(ids_block, start_pos) -> local logits handle (whatever ``gather`` takes)
     gather(local, counts) -> full logits [B, VS] on the root, None elsewhere
+    gather_ids(local, counts) -> (optional) greedy ids [B] on the root, None elsewhere: each
+        rank's argmax over its own rows, only the ids cross the links (SURVEY 8(e) option)
     """
 
     def __init__(self, world: int, rank: int, forward_local: Callable, gather: Callable,
-                 root: int = 0):
+                 root: int = 0, gather_ids: Optional[Callable] = None):
         self.world, self.rank, self.root = world, rank, root
         self.forward_local = forward_local
         self.gather = gather
+        self.gather_ids = gather_ids
 
     def __call__(self, input_ids, start_pos: int) -> Optional[np.ndarray]:
         ids = np.asarray(input_ids)
@@ -55,6 +58,21 @@ class ShardedPrefill:
         local = self.forward_local(ids[start:start + n], start_pos) if n else None
         full = self.gather(local, rows_per_rank(B, self.world))
         return None if full is None else full[:, None, :]
+
+    def greedy(self, input_ids, start_pos: int) -> Optional[np.ndarray]:
+        """Next greedy ids int64 ``[B, 1]`` on the root — ``np.argmax`` of the last-position
+        logits (llama3.py:320) — with only B ids gathered instead of B x VS logits; None
+        elsewhere."""
+        if self.gather_ids is None:
+            raise NotImplementedError("this ShardedPrefill was built without gather_ids")
+        ids = np.asarray(input_ids)
+        if ids.ndim != 2:
+            raise ValueError(f"input_ids must be [B, L], got {ids.shape}")
+        B = ids.shape[0]
+        start, n = shard_rows(B, self.world, self.rank)
+        local = self.forward_local(ids[start:start + n], start_pos) if n else None
+        full = self.gather_ids(local, rows_per_rank(B, self.world))
+        return None if full is None else np.asarray(full, dtype=np.int64).reshape(B, 1)
 
     @classmethod
     def on_device(cls, model, world: int, rank: int,
@@ -108,4 +126,14 @@ class ShardedPrefill:
             out = np.empty((total, VS), np.float32)
             return ctx.d2h(out, dst)
 
-        return cls(world, rank, forward_local, gather, root)
+        def gather_ids(local, counts):
+            total = sum(counts)
+            dst = buffer("gathered_ids", total * 4) if rank == root else None
+            src = local if local is not None else buffer("empty", 4)
+            ctx.gather_argmax(src, dst, counts, root)
+            if rank != root:
+                ctx.synchronize()
+                return None
+            return ctx.d2h(np.empty(total, np.int32), dst)
+
+        return cls(world, rank, forward_local, gather, root, gather_ids)

@@ -297,6 +297,10 @@ def test_sharded_prefill_world1_rccl(tmpdir_mod):
     got = sp(ids, 0)
     assert got.shape == want.shape
     np.testing.assert_array_equal(got, want)
+    # greedy ids only (SURVEY 8(e) option): device argmax per rank, int32 ids gathered
+    nxt = sp.greedy(ids, 0)
+    assert nxt.shape == (4, 1) and nxt.dtype == np.int64
+    np.testing.assert_array_equal(nxt[:, 0], np.argmax(want[:, 0, :], axis=-1))
 
 
 def test_gather_pipelined_forwards_world1(tmpdir_mod):

@@ -62,7 +62,15 @@ def _worker(rank, world, port, cases, outdir):
             return None
         return np.concatenate([o for o in objs if o is not None], axis=0)
 
-    sp = ShardedPrefill(world, rank, forward_local, gather)
+    def gather_ids(local, counts):  # the device path's per-rank argmax, then an ids gather
+        mine = None if local is None else np.argmax(local, axis=-1)
+        objs = [None] * world if rank == 0 else None
+        dist.gather_object(mine, objs, dst=0)
+        if rank != 0:
+            return None
+        return np.concatenate([o for o in objs if o is not None], axis=0)
+
+    sp = ShardedPrefill(world, rank, forward_local, gather, gather_ids=gather_ids)
     results = []
     for B, L, start in cases:
         ids = np.random.default_rng(B * 100 + L).integers(0, args.vocab_size, (B, L))
@@ -75,6 +83,13 @@ def _worker(rank, world, port, cases, outdir):
             results.append(bool(np.array_equal(out, want)) and out.shape == (B, 1, args.vocab_size))
         else:
             assert out is None
+        # greedy ids only (SURVEY 8(e) option): the same rows' argmax, ids gathered
+        nxt = sp.greedy(ids, start)
+        if rank == 0:
+            results.append(nxt.shape == (B, 1) and nxt.dtype == np.int64
+                           and bool(np.array_equal(nxt[:, 0], np.argmax(want[:, 0, :], axis=-1))))
+        else:
+            assert nxt is None
     dist.barrier()
     dist.destroy_process_group()
     if rank == 0:
