@@ -1089,7 +1089,11 @@ extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8
     CHECK_CTX(c);
     if (set_dev(c)) return 1;
     if (!c->comm_stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+        // high priority: a queue apart from the (normal-priority) forward streams, so the
+        // transfer does not serialize behind the next forward's kernels in a shared HW queue
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, greatest));
         HIP_TRY(hipEventCreateWithFlags(&c->comm_fwd_ev, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->comm_done_ev, hipEventDisableTiming));
     }
