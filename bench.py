@@ -329,6 +329,18 @@ def main():
     ctx.kernel_timing(False)
     ctx.set_batch_split(a.split if a.split is not None else 2)
 
+    # N > 1: the logits gather alone (untimed for `value`): its share of a step at this N,
+    # which the overlapped gather hides behind the next step's layers
+    gather_ms = None
+    if dist.world > 1:
+        dist.barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ctx.gather_logits(logits_dev, gathered_dev, rows, root=0)
+        ctx.synchronize()
+        gather_ms = dist.max(time.perf_counter() - t0) / a.steps * 1e3
+
     # the same forward with the logits copied back to host memory every step
     # (PCIe-inclusive; reported beside `value`, never as it)
     host_logits = np.empty((bpg, VS), np.float32)
@@ -370,6 +382,7 @@ def main():
         "ms_per_step_serialized": round(elapsed_serial / a.steps * 1e3, 4),
         "batch_split": a.split if a.split is not None else 2,
         "ms_per_step_with_logits_d2h": round(elapsed_d2h / d2h_steps * 1e3, 4),
+        "ms_gather_alone": None if gather_ms is None else round(gather_ms, 4),
         "higher_is_better": True,
         "scaling": "strong" if a.global_batch else "weak",
         "vs_baseline": None,
