@@ -129,3 +129,17 @@ def test_unique_id_file_exchange(tmp_path):
     got = [(tmp_path / f"uid{r}").read_bytes() for r in range(3)]
     assert got[0] == bytes(range(7, 135)) and got[1] == got[0] and got[2] == got[0]
     os.remove(os.path.join("/tmp", f"l3_rccl_uid_{key}"))
+
+
+def test_greedy_needs_gather_ids():
+    """ShardedPrefill.greedy (ids-only gather) refuses when built without gather_ids, and
+    checks the input rank like __call__."""
+    sp = ShardedPrefill(1, 0, lambda ids, s: ids, lambda local, counts: local)
+    with pytest.raises(NotImplementedError):
+        sp.greedy(np.zeros((2, 3), np.int64), 0)
+    sp = ShardedPrefill(1, 0, lambda ids, s: np.eye(4)[ids[:, -1]],
+                        lambda local, counts: local,
+                        gather_ids=lambda local, counts: np.argmax(local, axis=-1))
+    np.testing.assert_array_equal(sp.greedy(np.array([[0, 3], [1, 2]]), 0), [[3], [2]])
+    with pytest.raises(ValueError):
+        sp.greedy(np.zeros(3, np.int64), 0)
