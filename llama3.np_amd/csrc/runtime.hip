@@ -228,7 +228,7 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 9;  // bumped whenever a hot kernel changes (keys profiles/pmc_*.json)
+    if (minor) *minor = 10;  // bumped whenever a hot kernel changes (keys profiles/pmc_*.json)
     return 0;
 }
 
