@@ -24,7 +24,12 @@ the CUs, so a launch's duration would not measure the kernel): ms_per_step_seria
 traffic: HBM bytes per gate|up launch from the committed rocprofv3 PMC summary
 (profiles/pmc_gateup.json, FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction), or null.
 cpu_baseline: the oracle (NumPy restatement of the reference, oracle/) timed on
-this host's cores on a bounded sample (B=32, L=256), rank 0 at N=1 only.
+this host's cores on the C3 workload itself (B=256, L=256) per SURVEY 8(d): one warm-up
+forward, median of 3; rank 0 at N=1 only.
+Host path (ms_per_step_with_logits_d2h): Llama.__call__ on host ids, logits returned in a
+pinned NumPy array (l3hip.PinnedPool): ids H2D + forward + logits D2H, never `value`.
+N > 1 (or --rccl): after the timed region rank 0 recomputes every peer's seeded id block on
+its own context and compares it bit for bit with the gathered rows; a mismatch exits 3.
 """
 
 import argparse
@@ -53,18 +58,23 @@ class Dist:
     rank 0 -> peers through an atomically renamed file (single node, keyed by the launcher's
     pid and MASTER_PORT), and barriers / the max-over-ranks time run over RCCL itself."""
 
-    def __init__(self, n):
+    def __init__(self, n, force_comm=False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         if n != self.world:
             raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}; launch N>1 with torch.distributed.run")
         self.ctx = None
+        self.force_comm = force_comm
+
+    @property
+    def comm(self):
+        return self.world > 1 or self.force_comm
 
     def init_comm(self, ctx):
         self.ctx = ctx
-        if self.world > 1:
-            key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+        if self.world > 1 or self.force_comm:
+            key = uid_key()
             uid = l3hip.exchange_unique_id(self.rank, self.world, key)
             ctx.comm_init(self.world, self.rank, uid)
             ctx.comm_barrier()
@@ -75,37 +85,45 @@ class Dist:
                     pass
 
     def barrier(self):
-        if self.world > 1:
+        if self.comm:
             self.ctx.comm_barrier()
 
     def max(self, x):
-        return self.ctx.comm_max(x) if self.world > 1 else x
+        return self.ctx.comm_max(x) if self.comm else x
+
+
+def uid_key():
+    """Name of the RCCL-id hand-off file, equal on every rank of one launch: torchrun's run id
+    (TORCHELASTIC_RUN_ID, shared by the ranks of one launch) or else the launcher pid, plus
+    MASTER_PORT."""
+    run = os.environ.get("TORCHELASTIC_RUN_ID") or str(os.getppid())
+    return f"{run}_{os.environ.get('MASTER_PORT', '0')}"
 
 
 def cpu_baseline():
-    """Oracle (port of the reference's NumPy forward) on a bounded C3 sample."""
+    """Oracle (port of the reference's NumPy forward) on the C3 workload itself, SURVEY 8(d):
+    B=256, L=256, one warm-up forward, median of 3; plus a 1-thread figure on a B=4 sample."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import llama3_oracle as orc
 
     try:
         from threadpoolctl import threadpool_info
 
-        cores = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+        blas = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
     except Exception:
-        cores = int(os.environ.get("OPENBLAS_NUM_THREADS", os.cpu_count() or 1))
-    Bs = 32
+        blas = int(os.environ.get("OPENBLAS_NUM_THREADS", os.cpu_count() or 1))
+    Bs = B_PER_GPU
     args = synth.stories15m(Bs)
     w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=0)
     model = orc.OracleModel(w, args)
     ids = np.random.default_rng(1).integers(0, args.vocab_size, (Bs, SEQ))
-    model(ids[:4], 0)  # warm-up (small)
+    model(ids, 0)  # warm-up
     times = []
-    for _ in range(2):
+    for _ in range(3):
         t0 = time.perf_counter()
         model(ids, 0)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
-    # SURVEY 8(d) / BASELINE.md: a 1-thread figure beside the all-cores one (B = 4 sample)
     one = None
     try:
         from threadpoolctl import threadpool_limits
@@ -116,12 +134,14 @@ def cpu_baseline():
             one = round(4 * SEQ / (time.perf_counter() - t1), 1)
     except Exception:
         pass
-    return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(cores),
+    return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(blas),
+            "nproc": os.cpu_count(), "openblas_threads": int(blas),
             "value_1_thread": one,
             "kind": "port",
             "sample": f"oracle/llama3_oracle.py (NumPy restatement of the reference, f64 after layer-0 "
-                      f"RoPE as the reference) stories15M prefill B={Bs} L={SEQ}, median of 2 "
-                      f"({t:.2f} s each), OpenBLAS threads={cores}"}
+                      f"RoPE as the reference) stories15M prefill B={Bs} L={SEQ} (the C3 workload), "
+                      f"1 warm-up, median of 3 ({', '.join(f'{x:.2f}' for x in times)} s), "
+                      f"OpenBLAS threads={blas} of nproc={os.cpu_count()}; value_1_thread: B=4 sample"}
 
 
 def traffic_per_launch(rows):
@@ -130,8 +150,8 @@ def traffic_per_launch(rows):
         return None
     with open(p) as f:
         d = json.load(f)
-    if d.get("workload_rows") != rows or d.get("lib_version") != l3hip.version():
-        return None  # counters were measured on another build of the kernel
+    if d.get("workload_rows") != rows or d.get("source_hash") != l3hip.source_hash():
+        return None  # counters were measured on another build of the library
     return d.get("hbm_bytes_per_launch")
 
 
@@ -185,7 +205,23 @@ def bench_c5(a):
     ctx.synchronize()
     el = time.perf_counter() - t0
     st = ctx.kernel_stats()
+    ctx.kernel_timing(False)
     T = B * L
+    # outside the timed region: every logit finite, and row 0 equal to row 0 run alone (B = 1,
+    # same layer kernels; the B = 1 lm_head runs the GEMV, another reduction order over K = 4096,
+    # hence 1e-5 rather than bit equality — tests/test_gpu_parity.py measured 1.4e-5 at |logit| ~ 4)
+    out = np.empty((B, VS), np.float32)
+    ctx.d2h(out, logits_dev)
+    finite = bool(np.isfinite(out).all())
+    ctx.forward_dev(ids_dev, 1, L, 0, logits_dev)  # ids row 0 is the first L ids
+    row0 = np.empty((1, VS), np.float32)
+    ctx.d2h(row0, logits_dev)
+    row_err = float(np.max(np.abs(row0[0].astype(np.float64) - out[0])))
+    row_ok = bool(np.allclose(row0[0], out[0], rtol=1e-5, atol=1e-5))
+    if not (finite and row_ok):
+        print(json.dumps({"error": "c5 output check failed", "finite": finite,
+                          "row0_vs_alone_max_abs": row_err}), flush=True)
+        raise SystemExit(3)
     flops = {"qkv": 2.0 * T * D * (H + 2 * KVH) * HD, "oproj": 2.0 * T * D * D,
              "gateup": 2.0 * T * D * 2 * FD, "down": 2.0 * T * FD * D,
              "attn": 4.0 * HD * H * B * L * (L + 1) / 2, "lmhead": 2.0 * B * D * VS}
@@ -206,7 +242,9 @@ def bench_c5(a):
         "roofline": {"kernel": "gemm gate|up, M=131072 K=4096 N=28672", "bound": "mfma",
                      "achieved": gu, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(gu / PEAK_FP32_TFLOPS, 4), "traffic": None},
-        "kernels": per, "weight_upload_s": round(t_up, 1)}))
+        "kernels": per, "weight_upload_s": round(t_up, 1),
+        "output_check": {"all_finite": finite, "row0_vs_B1_run_max_abs": row_err, "tol": "1e-5 abs+rel"},
+        "lib": {"version": l3hip.version(), "source_hash": l3hip.source_hash()}}))
 
 
 def cpu_c5_slice():
@@ -240,6 +278,37 @@ def cpu_c5_slice():
         "unit": "tokens/s", "kind": "port", "cores": int(cores), "weight_gen_s": round(t_gen, 1)}))
 
 
+def check_gathered(ctx, dist, bpg, VS, gathered_dev):
+    """N > 1 self-check (untimed): rank 0 recomputes each peer's seeded id block (the same
+    default_rng(100 + r) draw the peer used) on its own context — same B, same kernels, so the
+    rows must be bit-identical — and compares them with the rows the RCCL gather delivered.
+    Returns the number of ranks checked; raises SystemExit(3) on a mismatch."""
+    if dist.rank != 0:
+        return None
+    got = np.empty((bpg * dist.world, VS), np.float32)
+    ctx.d2h(got, gathered_dev)  # joins the comm stream: the last gather has landed
+    ids_dev = ctx.alloc(bpg * SEQ * 4)
+    out_dev = ctx.alloc(bpg * VS * 4)
+    want = np.empty((bpg, VS), np.float32)
+    try:
+        for r in range(dist.world):
+            ids = np.random.default_rng(100 + r).integers(0, VS, (bpg, SEQ)).astype(np.int32)
+            ctx.h2d(ids_dev, ids)
+            ctx.forward_dev(ids_dev, bpg, SEQ, 0, out_dev)
+            ctx.d2h(want, out_dev)
+            blk = got[r * bpg:(r + 1) * bpg]
+            if not np.array_equal(blk, want):
+                bad = np.argwhere(blk != want)
+                print(json.dumps({"error": "gathered logits differ from rank 0's recomputation",
+                                  "rank": r, "mismatches": int(bad.shape[0]),
+                                  "first": bad[0].tolist()}), flush=True)
+                raise SystemExit(3)
+    finally:
+        ctx.free(ids_dev)
+        ctx.free(out_dev)
+    return dist.world
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,13 +325,16 @@ def main():
                     help="strong scaling: this many rows split over the GPUs (default: 256 per GPU)")
     ap.add_argument("--split", type=int, default=None,
                     help="batch-split parts of the timed forward (default: the library's, 2)")
+    ap.add_argument("--rccl", action="store_true",
+                    help="communicator, gather and self-check even at N=1 (rehearses the N>1 path "
+                         "under torch.distributed.run --nproc-per-node 1)")
     a = ap.parse_args()
     if a.workload == "c5":
         return bench_c5(a)
     if a.workload == "c5cpu":
         return cpu_c5_slice()
 
-    dist = Dist(a.gpus)
+    dist = Dist(a.gpus, force_comm=a.rccl)
     # default: weak scaling, B = 256 rows per GPU (N = 8 is C4's B = 2048); --global-batch G:
     # strong scaling, G rows split over the N GPUs (C4 at any N)
     if a.global_batch:
@@ -290,12 +362,12 @@ def main():
     gathered_dev = None
     rows = [bpg] * dist.world
     dist.init_comm(ctx)
-    if dist.world > 1 and dist.rank == 0:
+    if dist.comm and dist.rank == 0:
         gathered_dev = ctx.alloc(bpg * dist.world * VS * 4)
 
     def step():
         ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
-        if dist.world > 1:
+        if dist.comm:
             ctx.gather_logits(logits_dev, gathered_dev, rows, root=0)
 
     if a.split is not None:
@@ -318,6 +390,10 @@ def main():
     # value: the product forward (batch split into row ranges on concurrent streams), no events
     elapsed = timed_steps(a.steps)
 
+    # N > 1: the gathered rows against rank 0's own recomputation (untimed)
+    checked = check_gathered(ctx, dist, bpg, VS, gathered_dev) if dist.comm else None
+    dist.barrier()
+
     # roofline: the same K steps serialized (one row range, one stream) with HIP events around
     # the FFN GEMM launches only (12 per step) — with concurrent row ranges two kernels share
     # the CUs and a launch's duration no longer measures that kernel
@@ -332,7 +408,7 @@ def main():
     # N > 1: the logits gather alone (untimed for `value`): its share of a step at this N,
     # which the overlapped gather hides behind the next step's layers
     gather_ms = None
-    if dist.world > 1:
+    if dist.comm:
         dist.barrier()
         ctx.synchronize()
         t0 = time.perf_counter()
@@ -341,16 +417,18 @@ def main():
         ctx.synchronize()
         gather_ms = dist.max(time.perf_counter() - t0) / a.steps * 1e3
 
-    # the same forward with the logits copied back to host memory every step
-    # (PCIe-inclusive; reported beside `value`, never as it)
-    host_logits = np.empty((bpg, VS), np.float32)
+    # the drop-in host path, Llama.__call__ on host ids (int64) returning host
+    # logits (a pinned NumPy array): ids H2D + forward + logits D2H (PCIe-inclusive; reported
+    # beside `value`, never as it)
+    ids_host = ids.astype(np.int64)
     d2h_steps = max(1, min(a.steps, 10))
+    out = model(ids_host, 0)
+    del out
     dist.barrier()
-    ctx.synchronize()
     t0 = time.perf_counter()
     for _ in range(d2h_steps):
-        ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
-        ctx.d2h(host_logits, logits_dev)
+        out = model(ids_host, 0)
+        del out
     elapsed_d2h = dist.max(time.perf_counter() - t0)
 
     # sanity on the output (outside the timed region)
@@ -371,6 +449,7 @@ def main():
     achieved = gu_flops / gu_avg_s / 1e12
     ffn_tf = (gu_flops + dn_flops) / ((gu_ms / gu_n + dn_ms / dn_n) / 1e3) / 1e12
     traffic = traffic_per_launch(T)
+    host_ms = elapsed_d2h / d2h_steps * 1e3
     out = {
         "metric": METRIC,
         "value": round(tokens / elapsed, 1),
@@ -381,8 +460,10 @@ def main():
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "ms_per_step_serialized": round(elapsed_serial / a.steps * 1e3, 4),
         "batch_split": a.split if a.split is not None else 2,
-        "ms_per_step_with_logits_d2h": round(elapsed_d2h / d2h_steps * 1e3, 4),
+        "ms_per_step_with_logits_d2h": round(host_ms, 4),
+        "host_path_tokens_per_s": round(T * dist.world * d2h_steps / elapsed_d2h, 1),
         "ms_gather_alone": None if gather_ms is None else round(gather_ms, 4),
+        "gather_self_check_ranks": checked,
         "higher_is_better": True,
         "scaling": "strong" if a.global_batch else "weak",
         "vs_baseline": None,
@@ -391,6 +472,7 @@ def main():
         "config": {"workload": f"stories15M prefill, B={bpg} per GPU x L={SEQ}, start_pos 0",
                    "global_batch": bpg * dist.world, "seq_len": SEQ,
                    "parallelism": f"dp{dist.world} (batch rows) + RCCL logits gather"},
+        "lib": {"version": l3hip.version(), "source_hash": l3hip.source_hash()},
         "roofline": {"kernel": f"gemm gate|up (fused SwiGLU epilogue), M={T} K=288 N=1536",
                      "pass": "same workload and step count, batch split off (HIP events need "
                              "the kernel alone on the CUs)",

@@ -75,6 +75,9 @@ enum l3_kernel_id {
 const char* l3_last_error(void);
 int l3_device_count(int32_t* n);
 int l3_version(int32_t* major, int32_t* minor);
+/* sha256 prefix of the sources the library was built from (kernels, runtime, this header,
+ * the Makefile); bench lines and profile artefacts are keyed to it. */
+const char* l3_source_hash(void);
 
 /* ---- context (replaces Llama.__init__, llama3.py:265-283) ---------------- */
 /* n_layers may be 0 (op-only context); ctx owns all device memory. */
@@ -159,6 +162,13 @@ int l3_op_ffn_host(l3_ctx* ctx, const float* x, int64_t rows, int32_t dim, int32
 /* y [rows, N] = x [rows, K] @ W[N, K]^T (the reference's `x @ W.T`). */
 int l3_op_linear_host(l3_ctx* ctx, const float* x, int64_t rows, int32_t K, int32_t N,
                       const float* w, float* y);
+
+/* ---- pinned host memory (fast host-buffer path) ------------------------------ */
+/* Page-locked host allocation: l3_forward_host / l3_greedy_step_host / l3_d2h copying into
+ * it run as DMA at PCIe rate (the reference returns host logits, llama3.py:307-308; the
+ * Python binding hands these buffers out as the returned NumPy arrays).  Device-independent. */
+int l3_host_alloc(size_t bytes, void** ptr);
+int l3_host_free(void* ptr);
 
 /* ---- device memory helpers (bench: inputs resident in HBM) --------------- */
 int l3_dev_alloc(l3_ctx* ctx, size_t bytes, void** ptr);

@@ -349,6 +349,12 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         // wave issuing fewer would not wait for its own pieces of tile kt: stale LDS rows)
         constexpr int AP = BM / RP, BP = BN / RP;
         constexpr int GA_HI = (AP + 3) / 4, GA_LO = AP / 4, GB_HI = (BP + 3) / 4, GB_LO = BP / 4;
+        // the per-wave counts cover every piece exactly once: (AP % 4) waves issue GA_HI, the
+        // rest GA_LO (when AP % 4 == 0 all four issue GA_HI == GA_LO); same for B
+        static_assert((AP % 4) * GA_HI + (4 - AP % 4) * GA_LO == AP, "A pieces per wave");
+        static_assert((BP % 4) * GB_HI + (4 - BP % 4) * GB_LO == BP, "B pieces per wave");
+        static_assert(AP % 4 != 0 || GA_HI == GA_LO, "A pieces: equal counts");
+        static_assert(BP % 4 != 0 || GB_HI == GB_LO, "B pieces: equal counts");
         const bool a_hi = AP % 4 == 0 || wid < AP % 4, b_hi = BP % 4 == 0 || wid < BP % 4;
         auto wait_ring = [&]() {  // wave-uniform branches over compile-time counts
             if (a_hi) {

@@ -107,6 +107,8 @@ struct l3_ctx {
     int64_t ws_T = 0, ws_B = 0;
     float *h = nullptr, *q = nullptr, *attn = nullptr, *hid = nullptr, *logits = nullptr;
     int32_t *ids = nullptr, *amax = nullptr;
+    int32_t* ids_pin = nullptr;      // pinned host staging of the int32 ids (upload_ids)
+    int64_t ids_pin_n = 0;
     // op scratch
     std::vector<void*> scratch;
     // timing (bit k of timing_mask: record HIP events around launches of kernel id k)
@@ -228,9 +230,15 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 10;  // bumped whenever a hot kernel changes (keys profiles/pmc_*.json)
+    if (minor) *minor = 11;
     return 0;
 }
+
+#ifndef L3_SRC_HASH
+#define L3_SRC_HASH "unknown"
+#endif
+// sha256 prefix of the sources this library was built from (Makefile SRC_HASH)
+extern "C" const char* l3_source_hash(void) { return L3_SRC_HASH; }
 
 extern "C" int l3_device_count(int32_t* n) {
     int k = 0;
@@ -325,6 +333,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
     dfree(c->amax); dfree(c->gather_ids);
+    if (c->ids_pin) (void)hipHostFree(c->ids_pin);
     for (void* p : c->scratch) dfree(p);
     for (auto& t : c->timers) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     drop_decode_graph(c);
@@ -632,18 +641,29 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
     return rc;
 }
 
+// int64 host ids -> int32 device ids through a pinned staging buffer (a DMA copy, no pageable
+// bounce); the copy is ordered on stream before the forward, and the staging buffer is next
+// rewritten only by a later call, after this call's closing synchronize
 static int upload_ids(l3_ctx* c, const int64_t* ids_host, int64_t T) {
-    std::vector<int32_t> tmp((size_t)T);
+    if (T > c->ids_pin_n) {
+        if (c->ids_pin) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            HIP_TRY(hipHostFree(c->ids_pin));
+            c->ids_pin = nullptr;
+            c->ids_pin_n = 0;
+        }
+        HIP_TRY(hipHostMalloc(&c->ids_pin, (size_t)T * 4, hipHostMallocDefault));
+        c->ids_pin_n = T;
+    }
     const int64_t VS = c->d.vocab_size;
     for (int64_t i = 0; i < T; ++i) {
         int64_t v = ids_host[i];
         if (v < -VS || v >= VS)  // NumPy fancy indexing raises IndexError here (llama3.py:287)
             return fail("token id %lld out of range for vocab_size %lld", (long long)v, (long long)VS);
         if (v < 0) v += VS;  // ...and wraps negatives
-        tmp[(size_t)i] = (int32_t)v;
+        c->ids_pin[i] = (int32_t)v;
     }
-    HIP_TRY(hipMemcpyAsync(c->ids, tmp.data(), T * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));  // tmp goes out of scope
+    HIP_TRY(hipMemcpyAsync(c->ids, c->ids_pin, T * 4, hipMemcpyHostToDevice, c->stream));
     return 0;
 }
 
@@ -761,7 +781,9 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
     CHECK_CTX(c);
     const int steps = max_new_tokens - L;
     if (steps <= 0) return 0;
-    if (max_new_tokens - 1 > c->d.max_seq_len)
+    // the last decode step runs at position max_new_tokens - 1, which must be a cache slot
+    // (the reference fails there with a broadcast error, llama3.py:184)
+    if (max_new_tokens > c->d.max_seq_len)
         return fail("generate: last decode position %d exceeds max_seq_len %d", max_new_tokens - 1,
                     c->d.max_seq_len);
     std::vector<int64_t> first((size_t)B);
@@ -800,8 +822,10 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
         hipMemcpyAsync(hist + B, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
         return done(fail("generate: history copy failed"));
     if (steps > 2 && !set_hist(hist, L, steps)) return done(fail("generate: decode state update failed"));
+    // the graph replays only from the state the eager step above armed (position L + 2)
+    if (steps > 2 && (!c->dec_exec || c->dec_B != B || c->dec_pos_mirror != L + 2))
+        return done(fail("generate: decode graph not armed"));
     for (int i = 2; i < steps; ++i) {
-        if (!c->dec_exec || c->dec_B != B) return done(fail("generate: decode graph not armed"));
         if (hipGraphLaunch(c->dec_exec, c->stream) != hipSuccess)
             return done(fail("generate: graph replay failed"));
         c->graph_steps++;
@@ -1021,6 +1045,19 @@ extern "C" int l3_op_ffn_host(l3_ctx* c, const float* x, int64_t rows, int32_t d
 }
 
 // ---------------------------------------------------------------------------------------
+// pinned (page-locked) host memory: the copies of l3_forward_host / l3_d2h into it run as
+// DMA at PCIe rate instead of through a pageable bounce (l3hip hands such buffers out as the
+// NumPy arrays Llama.__call__ returns)
+extern "C" int l3_host_alloc(size_t bytes, void** ptr) {
+    if (!ptr) return fail("l3_host_alloc: null argument");
+    HIP_TRY(hipHostMalloc(ptr, bytes ? bytes : 4, hipHostMallocPortable));
+    return 0;
+}
+extern "C" int l3_host_free(void* ptr) {
+    if (ptr) HIP_TRY(hipHostFree(ptr));
+    return 0;
+}
+
 extern "C" int l3_dev_alloc(l3_ctx* c, size_t bytes, void** ptr) {
     CHECK_CTX(c);
     if (set_dev(c)) return 1;
@@ -1105,10 +1142,24 @@ extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8
     return 0;
 }
 
+// every rank's row count in [0, max_batch_size] (they size RCCL transfers and root offsets)
+static int check_rows(l3_ctx* c, const char* who, const int64_t* rows_per_rank, int32_t root) {
+    if (!rows_per_rank) return fail("%s: null rows_per_rank", who);
+    if (root < 0 || root >= c->nranks) return fail("%s: root %d outside [0, %d)", who, root, c->nranks);
+    const int64_t maxB = c->d.max_batch_size;
+    for (int r = 0; r < c->nranks; ++r)
+        if (rows_per_rank[r] < 0 || rows_per_rank[r] > maxB)
+            return fail("%s: rank %d has %lld rows, outside [0, max_batch_size %lld]", who, r,
+                        (long long)rows_per_rank[r], (long long)maxB);
+    return 0;
+}
+
 extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst_dev,
                                      const int64_t* rows_per_rank, int32_t root) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_gather_logits: communicator not initialised");
+    if (check_rows(c, "l3_comm_gather_logits", rows_per_rank, root)) return 1;
+    if (c->rank == root && !dst_dev) return fail("l3_comm_gather_logits: null destination on the root");
     if (set_dev(c, false)) return 1;
     const int64_t VS = c->d.vocab_size;
     // on comm_stream after everything queued so far on stream (the forward that wrote src);
@@ -1153,11 +1204,10 @@ extern "C" int l3_comm_gather_argmax(l3_ctx* c, const float* src_dev, int32_t* d
                                      const int64_t* rows_per_rank, int32_t root) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_gather_argmax: communicator not initialised");
+    if (check_rows(c, "l3_comm_gather_argmax", rows_per_rank, root)) return 1;
+    if (c->rank == root && !dst_dev) return fail("l3_comm_gather_argmax: null destination on the root");
     if (set_dev(c)) return 1;
     const int64_t n = rows_per_rank[c->rank], maxB = c->d.max_batch_size;
-    if (n < 0 || n > maxB)
-        return fail("l3_comm_gather_argmax: %lld rows on this rank, max_batch_size %lld",
-                    (long long)n, (long long)maxB);
     if (!c->gather_ids) HIP_TRY(hipMalloc(&c->gather_ids, (maxB > 0 ? maxB : 1) * 4));
     if (n) HIP_TRY(launch_argmax(src_dev, n, (int)c->d.vocab_size, c->gather_ids, c->stream));
     NCCL_TRY(ncclGroupStart());

@@ -48,6 +48,9 @@ _SIGNATURES = {
     "l3_last_error": (ctypes.c_char_p, []),
     "l3_device_count": (ctypes.c_int, [_P]),
     "l3_version": (ctypes.c_int, [_P, _P]),
+    "l3_source_hash": (ctypes.c_char_p, []),
+    "l3_host_alloc": (ctypes.c_int, [_SZ, _P]),
+    "l3_host_free": (ctypes.c_int, [_P]),
     "l3_create": (ctypes.c_int, [_I32, _P, _P]),
     "l3_destroy": (ctypes.c_int, [_P]),
     "l3_upload_weight": (ctypes.c_int, [_P, _I32, _I32, _P, _I64, _I64]),
@@ -125,6 +128,56 @@ def version() -> str:
     return f"{major.value}.{minor.value}"
 
 
+def source_hash() -> str:
+    """sha256 prefix of the sources the loaded library was built from (keys profiles)."""
+    return lib().l3_source_hash().decode()
+
+
+class PinnedPool:
+    """Page-locked host buffers handed out as NumPy arrays (``l3_host_alloc``).
+
+    The library's host-path copies (logits D2H of ``Llama.__call__``) run as DMA at PCIe
+    rate into such a buffer instead of through a pageable bounce.  The array owns its
+    block through a ctypes buffer object; once the array and every view of it are gone the
+    block returns to a free list and the next call of the same size reuses it (at most
+    ``keep`` free blocks are kept, the rest are freed)."""
+
+    def __init__(self, keep: int = 4):
+        import threading
+
+        self.keep = keep
+        self._free = {}  # nbytes -> [address]
+        self._lock = threading.Lock()
+
+    def empty(self, shape, dtype) -> np.ndarray:
+        import weakref
+
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+        nb = max(n, 64)
+        with self._lock:
+            blocks = self._free.get(nb)
+            addr = blocks.pop() if blocks else None
+        if addr is None:
+            p = ctypes.c_void_p()
+            check(lib().l3_host_alloc(nb, ctypes.byref(p)))
+            addr = p.value
+        holder = (ctypes.c_char * nb).from_address(addr)
+        weakref.finalize(holder, self._release, addr, nb)
+        return np.frombuffer(holder, dtype=dtype, count=n // dtype.itemsize).reshape(shape)
+
+    def _release(self, addr: int, nb: int) -> None:
+        with self._lock:
+            blocks = self._free.setdefault(nb, [])
+            if len(blocks) < self.keep:
+                blocks.append(addr)
+                return
+        lib().l3_host_free(addr)
+
+
+pinned = PinnedPool()
+
+
 def device_count() -> int:
     n = ctypes.c_int32(0)
     check(lib().l3_device_count(ctypes.byref(n)))
@@ -171,7 +224,7 @@ class Context:
     def forward(self, ids: np.ndarray, start_pos: int) -> np.ndarray:
         ids = np.ascontiguousarray(ids, dtype=np.int64)
         B, L = ids.shape
-        out = np.empty((B, self.dims.vocab_size), np.float32)
+        out = pinned.empty((B, self.dims.vocab_size), np.float32)  # DMA target of the D2H
         check(lib().l3_forward_host(self._h, ptr(ids), B, L, start_pos, ptr(out)))
         return out
 
@@ -179,7 +232,7 @@ class Context:
         ids = np.ascontiguousarray(ids, dtype=np.int64)
         B, L = ids.shape
         nxt = np.empty(B, np.int64)
-        logits = np.empty((B, self.dims.vocab_size), np.float32) if want_logits else None
+        logits = pinned.empty((B, self.dims.vocab_size), np.float32) if want_logits else None
         check(lib().l3_greedy_step_host(self._h, ptr(ids), B, L, start_pos, ptr(nxt),
                                         ptr(logits) if logits is not None else None))
         return nxt, logits
@@ -252,15 +305,25 @@ class Context:
     def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().l3_comm_init(self._h, nranks, rank, buf))
+        self.nranks, self.rank = nranks, rank
+
+    def _rows(self, rows_per_rank) -> np.ndarray:
+        rows = np.ascontiguousarray(rows_per_rank, dtype=np.int64)
+        n = getattr(self, "nranks", None)
+        if n is None:
+            raise RuntimeError("communicator not initialised (comm_init)")
+        if rows.shape != (n,):
+            raise ValueError(f"rows_per_rank has {rows.size} entries, the communicator {n} ranks")
+        return rows
 
     def gather_logits(self, src_dev: int, dst_dev: Optional[int], rows_per_rank, root: int = 0):
-        rows = np.ascontiguousarray(rows_per_rank, dtype=np.int64)
+        rows = self._rows(rows_per_rank)
         check(lib().l3_comm_gather_logits(self._h, src_dev, dst_dev or 0, ptr(rows), root))
 
     def gather_argmax(self, src_dev: int, dst_dev: Optional[int], rows_per_rank, root: int = 0):
         """Greedy ids only: each rank's argmax over its logits rows, int32 ids gathered to
         ``dst_dev`` [sum rows] on the root (SURVEY 8(e) option)."""
-        rows = np.ascontiguousarray(rows_per_rank, dtype=np.int64)
+        rows = self._rows(rows_per_rank)
         check(lib().l3_comm_gather_argmax(self._h, src_dev, dst_dev or 0, ptr(rows), root))
 
     def comm_barrier(self) -> None:

@@ -18,6 +18,11 @@ Differences from the reference, all deliberate:
   callers always pass exactly those (``llama3.py:289-297``); shapes are checked.
 * ``compute_cos_sin_cache`` stays a host function (init-time f64 tables, as
   ``llama3.py:31-38``); the device builds its own fp32 copy of the same table.
+* the module functions ``softmax``, ``silu``, ``apply_rotary_emb``, ``repeat_kv``
+  and ``RMSNorm.__call__`` are host NumPy with the reference's exact semantics
+  (dtype kept, results bit-identical): the forward never calls them — its
+  versions are fused into the kernels — and the reference's own tests check
+  them with ``==``.
 
 Everything the reference keeps on the object (``args``, ``tok_embedding``,
 ``freqs_cos/sin``, ``layers``, ``norm``, ``lm_head_weight``, per-class weight
@@ -42,17 +47,24 @@ DEFAULT_DEVICE = int(os.environ.get("LLAMA3_HIP_DEVICE", "0"))
 
 
 # ---- module functions (reference llama3.py:22-83) ----------------------------
+#
+# Host NumPy, as in the reference, so the module API keeps its exact semantics: the input
+# dtype is kept (an f64 masked-score array stays f64) and the results are bit-identical to the
+# reference's (its own suite compares them with ==, tests/test_llama_implementations.py:55-111;
+# here tests/test_module_api.py against the reference-generated tests/golden/ops.npz).  The
+# device forward never calls them: there the same arithmetic is fused into the HIP kernels
+# (softmax and mask in attn_fwd_kernel, RoPE in the QKV GEMM epilogue, RMSNorm as a row factor
+# of the consuming GEMM); the standalone GPU op kernels stay reachable as l3hip.Context.op_*.
 
 def softmax(x):
-    """Row softmax over the last axis on the GPU (reference llama3.py:22-24)."""
-    x = np.asarray(x)
-    return l3hip.op_context(DEFAULT_DEVICE).op_softmax(x).reshape(x.shape)
+    """Row softmax over the last axis, input dtype kept (reference llama3.py:22-24)."""
+    e = np.exp(x - np.max(x, axis=-1, keepdims=True))
+    return e / np.sum(e, axis=-1, keepdims=True)
 
 
 def silu(x):
-    """x * sigmoid(x) on the GPU (reference llama3.py:27-28)."""
-    x = np.asarray(x)
-    return l3hip.op_context(DEFAULT_DEVICE).op_silu(x).reshape(x.shape)
+    """x * (1 / (1 + exp(-x))), input dtype kept (reference llama3.py:27-28)."""
+    return x * (1 / (1 + np.exp(-x)))
 
 
 def compute_cos_sin_cache(head_dim: int, max_seq_len: int, base: int = 10000):
@@ -62,10 +74,20 @@ def compute_cos_sin_cache(head_dim: int, max_seq_len: int, base: int = 10000):
     return np.cos(ang), np.sin(ang)
 
 
+def _rotate_pairs(x, c, s):
+    """(x[2i], x[2i+1]) rotated by the angle whose cos / sin are c / s (broadcast [1,L,1,HD/2])."""
+    pairs = x.reshape(x.shape[:-1] + (-1, 2))
+    re, im = pairs[..., 0], pairs[..., 1]
+    out = np.stack([re * c - im * s, re * s + im * c], axis=-1)
+    return out.reshape(out.shape[:-2] + (-1,))
+
+
 def apply_rotary_emb(xq, xk, freqs_cos, freqs_sin):
-    """Interleaved-pair RoPE of q and k on the GPU (reference llama3.py:41-76)."""
-    ctx = l3hip.op_context(DEFAULT_DEVICE)
-    return ctx.op_rope(xq, freqs_cos, freqs_sin), ctx.op_rope(xk, freqs_cos, freqs_sin)
+    """Interleaved-pair RoPE of q and k (reference llama3.py:41-76); the result takes the
+    promoted dtype of the inputs and tables (f64 with the reference's f64 tables)."""
+    c = np.expand_dims(freqs_cos, axis=(0, 2))
+    s = np.expand_dims(freqs_sin, axis=(0, 2))
+    return _rotate_pairs(xq, c, s), _rotate_pairs(xk, c, s)
 
 
 def repeat_kv(x, n_rep: int):
@@ -110,7 +132,15 @@ class _Dropped:
 
 class FeedForward:
     """SwiGLU MLP (reference llama3.py:86-103): one fused gate|up MFMA GEMM with a
-    silu(g)*u epilogue, then the down GEMM."""
+    silu(g)*u epilogue, then the down GEMM, on the GPU.
+
+    Unlike the module functions above this stays a device call: it is the metric's kernel
+    pair, and a standalone call is how a user reaches it outside a whole
+    forward.  The arithmetic is fp32 (as the forward); the result is returned in the dtype
+    the reference's ``x @ W`` would produce (``np.result_type(x, W)``), so the reference's
+    dtype contract holds, but the values match it to fp32 tolerance, not bit for bit (the
+    reference's own suite pins FeedForward only through the full forward at 1e-4,
+    tests/test_llama_implementations.py:114-179)."""
 
     def __init__(self, up_weight, gate_weight, down_weight):
         self.up_weight = up_weight.T
@@ -122,19 +152,22 @@ class FeedForward:
         ctx = l3hip.op_context(DEFAULT_DEVICE)
         y = ctx.op_ffn(x.reshape(-1, x.shape[-1]), self.gate_weight.T, self.up_weight.T,
                        self.down_weight.T)
-        return y.reshape(x.shape)
+        out_t = np.result_type(x.dtype, self.gate_weight.dtype, self.down_weight.dtype)
+        return y.reshape(x.shape).astype(out_t, copy=False)
 
 
 class RMSNorm:
-    """x / sqrt(mean(x^2) + eps) * w (reference llama3.py:106-114)."""
+    """x / sqrt(mean(x^2) + eps) * w on the host, input dtype kept (reference
+    llama3.py:106-114; bit-identical to it, see the module functions' note).  Inside the
+    device forward the norm is a row factor of the consuming GEMM."""
 
     def __init__(self, weight, eps: float):
         self.weight = weight
         self.eps = eps
 
     def __call__(self, x):
-        x = np.asarray(x)
-        return l3hip.op_context(DEFAULT_DEVICE).op_rmsnorm(x, self.weight, self.eps).reshape(x.shape)
+        z = (x ** 2).mean(-1, keepdims=True) + self.eps
+        return (x / np.sqrt(z)) * self.weight
 
 
 class Attention:

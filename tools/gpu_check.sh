@@ -40,7 +40,10 @@ for s in "$@"; do
     c5small1) L3_BATCH_SPLIT=1 step c5small1 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
     rccl1) step rccl1 180 python tools/rccl_selftest.py --world 1 ;;
-    torchrun1) step torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline ;;
+    torchrun1) step torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline --rccl ;;
+    pmcattn) step pmcattnA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcattnA -o run --output-format csv -- tools/attn_tune 1 2 c3
+           step pmcattnB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcattnB -o run --output-format csv -- tools/attn_tune 1 2 c3 ;;
+    attnprof) step attnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attnprof -o run --output-format csv -- tools/attn_tune 3 10 ;;
     cabi) step cabi 300 python -u -m pytest tests/test_c_abi_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
