@@ -582,8 +582,11 @@ static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipSt
 // c->split row ranges on their own streams and one range's kernels fill another's launch tails
 // and kernel boundaries (C3: 7.31 -> 7.04 ms/step at 2 parts; 3 and 4 parts are slower).
 
+// logits_host (optional): each part's rows are copied back on that part's own stream right
+// after its lm_head, so part 0's D2H overlaps part 1's last layer and the parts' copies run
+// concurrently (two DMA queues); the join below covers them
 static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
-                       float* logits_dev, const int* pos_dev = nullptr) {
+                       float* logits_dev, const int* pos_dev = nullptr, float* logits_host = nullptr) {
     // roctx ranges (host-side launch spans; `rocprofv3 --marker-trace`) per block and lm_head
     static const char* names[] = {"l3.layer0", "l3.layer1", "l3.layer2", "l3.layer3", "l3.layer4",
                                   "l3.layer5", "l3.layer6", "l3.layer7", "l3.layerN"};
@@ -627,15 +630,39 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
         for (int p = 0; p < (lm_parts ? parts : 1); ++p) HIP_TRY(hipStreamWaitEvent(st[p], c->comm_done_ev, 0));
         c->gather_pending = false;
     }
+    const int64_t VS = c->d.vocab_size;
+    auto d2h_rows = [&](int r0, int n, hipStream_t s) -> int {
+        if (!logits_host || !n) return 0;
+        HIP_TRY(hipMemcpyAsync(logits_host + (int64_t)r0 * VS, logits_dev + (int64_t)r0 * VS,
+                               (size_t)n * VS * 4, hipMemcpyDeviceToHost, s));
+        return 0;
+    };
     roctxRangePushA("l3.lm_head");
-    for (int p = 0; p < parts && lm_parts && !rc; ++p) rc = run_lm_head(c, nb[p], L, logits_dev, b0[p], st[p]);
+    for (int p = 0; p < parts && lm_parts && !rc; ++p) {
+        rc = run_lm_head(c, nb[p], L, logits_dev, b0[p], st[p]);
+        if (!rc) rc = d2h_rows(b0[p], nb[p], st[p]);
+    }
     roctxRangePop();
     for (int p = 1; p < parts; ++p) {  // stream waits for every part: later calls see all rows
         HIP_TRY(hipEventRecord(c->join_ev[p - 1], st[p]));
         HIP_TRY(hipStreamWaitEvent(c->stream, c->join_ev[p - 1], 0));
     }
     roctxRangePushA("l3.lm_head");
-    if (!rc && !lm_parts) rc = run_lm_head(c, B, L, logits_dev, 0, c->stream);
+    if (!rc && !lm_parts) {
+        rc = run_lm_head(c, B, L, logits_dev, 0, c->stream);
+        // one lm_head for the batch: its rows still go back as two concurrent copies
+        if (!rc && logits_host && B >= 2 && !pos_dev) {
+            const int h = B / 2;
+            HIP_TRY(hipEventRecord(c->fork_ev, c->stream));
+            HIP_TRY(hipStreamWaitEvent(c->aux[0], c->fork_ev, 0));
+            rc = d2h_rows(0, h, c->stream);
+            if (!rc) rc = d2h_rows(h, B - h, c->aux[0]);
+            HIP_TRY(hipEventRecord(c->join_ev[0], c->aux[0]));
+            HIP_TRY(hipStreamWaitEvent(c->stream, c->join_ev[0], 0));
+        } else if (!rc) {
+            rc = d2h_rows(0, B, c->stream);
+        }
+    }
     roctxRangePop();
     roctxRangePop();
     return rc;
@@ -690,9 +717,7 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
     CHECK_CTX(c);
     if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
     if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
-    if (forward_dev(c, c->ids, B, L, start_pos, c->logits)) return 1;
-    HIP_TRY(hipMemcpyAsync(logits_host, c->logits, (int64_t)B * c->d.vocab_size * 4,
-                           hipMemcpyDeviceToHost, c->stream));
+    if (forward_dev(c, c->ids, B, L, start_pos, c->logits, nullptr, logits_host)) return 1;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return 0;
 }
@@ -1130,7 +1155,10 @@ extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8
         // transfer does not serialize behind the next forward's kernels in a shared HW queue
         int least = 0, greatest = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, greatest));
+        // L3_COMM_PRIORITY=0: normal priority (A/B of the queue placement)
+        const char* pe = getenv("L3_COMM_PRIORITY");
+        const int prio = (pe && pe[0] == '0') ? least : greatest;
+        HIP_TRY(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
         HIP_TRY(hipEventCreateWithFlags(&c->comm_fwd_ev, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->comm_done_ev, hipEventDisableTiming));
     }

@@ -35,14 +35,21 @@ struct Variant {
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, dim3(256), 0, s, a); \
             }}
 
+#define AVAR2(HD, QBW, G, KT, WPE)                                                            \
+    Variant{"v2<" #HD ",q" #QBW ",g" #G ",kt" #KT ",w" #WPE ">", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * (4 / G);                                        \
+                dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
+                hipLaunchKernelGGL((attn_fwd_v2_kernel<HD, QBW, G, KT, WPE>), grid, dim3(256), 0, s, a); \
+            }}
+
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
     for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;
 }
 
 static void run(const char* label, int B, int L, int H, int KVH, int HD, std::vector<Variant> vars,
-                int rounds, int iters) {
-    const int Smax = L;
+                int rounds, int iters, int start_pos = 0) {
+    const int Smax = start_pos + L;
     const size_t nq = (size_t)B * L * H * HD, nkv = (size_t)B * KVH * Smax * HD;
     std::vector<float> hq(nq), hk(nkv), hv(nkv);
     fill(hq, -1.f, 1.f, 1);
@@ -55,8 +62,8 @@ static void run(const char* label, int B, int L, int H, int KVH, int HD, std::ve
     CK(hipMemcpy(v, hv.data(), nkv * 4, hipMemcpyHostToDevice));
     AttnArgs a{};
     a.q = q; a.cache_k = k; a.cache_v = v; a.out = o;
-    a.B = B; a.L = L; a.start_pos = 0; a.H = H; a.KVH = KVH; a.HD = HD; a.Smax = Smax;
-    const double flops = 4.0 * HD * H * (double)B * L * (L + 1) / 2;  // causal useful half
+    a.B = B; a.L = L; a.start_pos = start_pos; a.H = H; a.KVH = KVH; a.HD = HD; a.Smax = Smax;
+    const double flops = 4.0 * HD * H * (double)B * L * ((L + 1) / 2.0 + start_pos);  // causal useful part
     printf("\n== %s B=%d L=%d H=%d KVH=%d HD=%d (%.2f GFLOP useful)\n", label, B, L, H, KVH, HD, flops / 1e9);
     std::vector<float> ref(nq), got(nq);
     for (size_t i = 0; i < vars.size(); ++i) {
@@ -98,6 +105,17 @@ int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
     if (argc > 3 && std::string(argv[3]) == "c3") {  // the product C3 kernel alone (PMC passes)
         run("stories15M C3", 256, 256, 6, 6, 48, {AVAR(48, 4, 1, 64)}, rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "v2") {  // v2 (per-key-group chains) against v1
+        run("stories15M C3", 256, 256, 6, 6, 48,
+            {AVAR(48, 4, 1, 64), AVAR2(48, 4, 1, 64, 2), AVAR2(48, 4, 1, 32, 2), AVAR2(48, 4, 1, 64, 1)},
+            rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48,
+            {AVAR(48, 4, 1, 64), AVAR2(48, 4, 1, 64, 2)}, 1, 1, 37);
+        run("stories15M L=100", 16, 100, 6, 6, 48, {AVAR(48, 4, 1, 64), AVAR2(48, 4, 1, 64, 2)}, 1, 1);
+        run("Llama-3 shape (C5 slice)", 4, 2048, 32, 8, 128,
+            {AVAR(128, 1, 4, 32), AVAR2(128, 1, 4, 32, 2)}, rounds, 3);
         return 0;
     }
     run("stories15M C3", 256, 256, 6, 6, 48,
