@@ -325,6 +325,8 @@ def main():
                     help="strong scaling: this many rows split over the GPUs (default: 256 per GPU)")
     ap.add_argument("--split", type=int, default=None,
                     help="batch-split parts of the timed forward (default: the library's, 2)")
+    ap.add_argument("--no-step-gather", action="store_true",
+                    help="diagnostic: communicator up but no gather inside the timed steps")
     ap.add_argument("--rccl", action="store_true",
                     help="communicator, gather and self-check even at N=1 (rehearses the N>1 path "
                          "under torch.distributed.run --nproc-per-node 1)")
@@ -365,9 +367,11 @@ def main():
     if dist.comm and dist.rank == 0:
         gathered_dev = ctx.alloc(bpg * dist.world * VS * 4)
 
+    step_gather = dist.comm and not a.no_step_gather
+
     def step():
         ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
-        if dist.comm:
+        if step_gather:
             ctx.gather_logits(logits_dev, gathered_dev, rows, root=0)
 
     if a.split is not None:
@@ -391,7 +395,7 @@ def main():
     elapsed = timed_steps(a.steps)
 
     # N > 1: the gathered rows against rank 0's own recomputation (untimed)
-    checked = check_gathered(ctx, dist, bpg, VS, gathered_dev) if dist.comm else None
+    checked = check_gathered(ctx, dist, bpg, VS, gathered_dev) if step_gather else None
     dist.barrier()
 
     # roofline: the same K steps serialized (one row range, one stream) with HIP events around

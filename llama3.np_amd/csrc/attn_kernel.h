@@ -34,7 +34,12 @@ namespace l3 {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int HD, int QBW, int G, int KT>
+// ABL: ablation bits for tools/attn_tune timing studies only (product launches use 0; results
+// are wrong with any bit set): 1 every tile full and unmasked for every block (no causal
+// structure), 2 p = s (no exp), 4 no K/V loads after tile 0, 8 no barrier in the tile loop,
+// 16 no softmax bookkeeping (no max / rescale / sum); 32 (timing study, results correct): K/V
+// tiles prefetched two ahead through two register sets
+template <int HD, int QBW, int G, int KT, int ABL = 0>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (G == 1 || G == 2 || G == 4), "shape");
     constexpr int WPH = 4 / G;                // waves per head
@@ -93,7 +98,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
 
     const int64_t kv_base = ((int64_t)b * p.KVH + kvh) * p.Smax;
     f32x4 rk[K_IT], rv[K_IT];
-    auto gload = [&](int tile) {
+    f32x4 rk2[(ABL & 32) ? K_IT : 1], rv2[(ABL & 32) ? K_IT : 1];
+    auto gload_into = [&](int tile, f32x4* dk, f32x4* dv) {
 #pragma unroll
         for (int i = 0; i < K_IT; ++i) {
             const int f = tid + 256 * i;
@@ -104,28 +110,40 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 vk = *reinterpret_cast<const f32x4*>(p.cache_k + (kv_base + key) * HD + c);
                 vv = *reinterpret_cast<const f32x4*>(p.cache_v + (kv_base + key) * HD + c);
             }
-            rk[i] = vk;
-            rv[i] = vv;
+            dk[i] = vk;
+            dv[i] = vv;
         }
     };
-    auto sstore = [&](int buf) {
+    auto sstore_from = [&](int buf, const f32x4* sk, const f32x4* sv) {
 #pragma unroll
         for (int i = 0; i < K_IT; ++i) {
             const int f = tid + 256 * i;
             if (K_F4 % 256 == 0 || f < K_F4) {
                 const int row = f / (HD / 4), c = (f % (HD / 4)) * 4;
-                *reinterpret_cast<f32x4*>(&Ks[buf][row][c]) = rk[i];
-                *reinterpret_cast<f32x4*>(&Vs[buf][row][c]) = rv[i];
+                *reinterpret_cast<f32x4*>(&Ks[buf][row][c]) = sk[i];
+                *reinterpret_cast<f32x4*>(&Vs[buf][row][c]) = sv[i];
             }
         }
     };
+    auto gload = [&](int tile) { gload_into(tile, rk, rv); };
+    auto sstore = [&](int buf) { sstore_from(buf, rk, rv); };
 
     gload(0);
     sstore(0);
+    if constexpr ((ABL & 32) != 0) {
+        if (ntiles > 1) gload(1);  // set A holds tile 1
+    }
     __syncthreads();
     for (int tile = 0; tile < ntiles; ++tile) {
         const int cur = tile & 1;
-        if (tile + 1 < ntiles) gload(tile + 1);
+        if constexpr ((ABL & 32) != 0) {  // tile + 2 into the set that held tile (its store is done)
+            if (tile + 2 < ntiles) {
+                if (tile & 1) gload_into(tile + 2, rk, rv);
+                else gload_into(tile + 2, rk2, rv2);
+            }
+        } else if (!(ABL & 4) && tile + 1 < ntiles) {
+            gload(tile + 1);
+        }
         const int k0 = tile * KT;
         {
             // one q-block against this K/V tile; MASKED: the diagonal tile (some key of the tile
@@ -166,6 +184,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                         sacc[kg][r] = v;
                         mt = fmaxf(mt, v);
                     }
+                if constexpr (!(ABL & 16)) {
                 mt = max_xor16_32(mt);
                 const float m_new = fmaxf(m_run[j], mt);
                 // v_exp_f32 directly: arguments are <= 0 (exact 0 at -inf), so the libm
@@ -177,13 +196,15 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 for (int kg = 0; kg < KG; ++kg)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float pv = __builtin_amdgcn_exp2f(sacc[kg][r] - m_new);
+                        const float pv = (ABL & 2) ? sacc[kg][r] - m_new
+                                                   : __builtin_amdgcn_exp2f(sacc[kg][r] - m_new);
                         sacc[kg][r] = pv;
                         psum += pv;
                     }
                 l_run[j] = l_run[j] * alpha + psum;
 #pragma unroll
                 for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;
+                }
 #pragma unroll
                 for (int kg = 0; kg < KG; ++kg) {
                     if (!live[kg]) continue;
@@ -201,16 +222,23 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 const int qblock_first = q_lo + qblk[j] * 16;
                 if (qblock_first >= p.L) continue;                        // padding block
                 const int qmax_abs = start_pos + min(qblock_first + 15, p.L - 1);
-                if (k0 > qmax_abs) continue;                              // whole tile masked
+                if (!(ABL & 1) && k0 > qmax_abs) continue;                // whole tile masked
                 // every key of the tile <= every query of the block: no mask, all groups live
-                if (k0 + KT - 1 <= start_pos + qblock_first)
+                if ((ABL & 1) || k0 + KT - 1 <= start_pos + qblock_first)
                     qblock_tile(j, qblock_first, qmax_abs, std::integral_constant<bool, false>{});
                 else
                     qblock_tile(j, qblock_first, qmax_abs, std::integral_constant<bool, true>{});
             }
         }
-        if (tile + 1 < ntiles) sstore(cur ^ 1);
-        __syncthreads();
+        if constexpr ((ABL & 32) != 0) {
+            if (tile + 1 < ntiles) {
+                if (tile & 1) sstore_from(cur ^ 1, rk2, rv2);
+                else sstore_from(cur ^ 1, rk, rv);
+            }
+        } else if (!(ABL & 4) && tile + 1 < ntiles) {
+            sstore(cur ^ 1);
+        }
+        if constexpr (!(ABL & 8)) __syncthreads();
     }
 
     // finalize: l = sum over the 4 lane groups; lane holds O^T[d = dg*16 + fk + r][q = fq]

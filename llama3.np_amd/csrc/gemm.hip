@@ -57,6 +57,8 @@ bool gemm_is_gemv(const GemmArgs& a) {
     return short_m && (size_t)mr * a.K <= 16384;  // A rows fit 64 KB of LDS (QKV: N even)
 }
 
+// ids compare rounding: 3 and 4 (128 x 128 vs 256 x 64 tiles) visit K in the same order per
+// element (BK 16, one MFMA chain per accumulator), so they round identically
 int gemm_store_config(const GemmArgs& a) {
     if (gemm_is_gemv(a)) return 0;
     return a.M <= 32 ? 1 : a.M <= 64 ? 2 : 3;
@@ -102,7 +104,12 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
             switch (gemm_store_config(a)) {
                 case 1: return launch<EPI_STORE, 2, 2, 1, 4, 2, 16, 6>(a, s);
                 case 2: return launch<EPI_STORE, 2, 2, 2, 4, 2, 16, 6>(a, s);
-                default: return launch<EPI_STORE, 2, 2, 4, 4, 2, 16, 4>(a, s);
+                default:
+                    // 129-256 rows: one 256-row panel per column tile, so the weight streams from
+                    // HBM once per launch (two 128-row tiles read it twice: 1.54x the algorithmic
+                    // bytes at B = 256, profiles/pmc_gateup.json r01)
+                    if (a.M > 128 && a.M <= 256) return launch<EPI_STORE, 4, 1, 4, 4, 2, 16, 3>(a, s);
+                    return launch<EPI_STORE, 2, 2, 4, 4, 2, 16, 4>(a, s);
             }
         default:
             return hipErrorInvalidValue;

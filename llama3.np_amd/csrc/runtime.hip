@@ -1190,11 +1190,19 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
     if (c->rank == root && !dst_dev) return fail("l3_comm_gather_logits: null destination on the root");
     if (set_dev(c, false)) return 1;
     const int64_t VS = c->d.vocab_size;
-    // on comm_stream after everything queued so far on stream (the forward that wrote src);
-    // a previous gather is ordered before it by comm_stream itself
-    HIP_TRY(hipEventRecord(c->comm_fwd_ev, c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->comm_fwd_ev, 0));
-    hipStream_t s = c->comm_stream;
+    // Default (mode 1): on the context stream, after the forward that wrote src and before the
+    // next one — no cross-stream events.  The overlapped form (mode 0, L3_COMM_MODE=0: the
+    // transfer on the high-priority comm stream, ordered by events, the next lm_head waiting for
+    // it) measured 7.96 ms/step against 6.94 at world 1 on MI355X, and 7.97 still with the
+    // comm stream left empty (mode 2: root's own rows on the context stream) — the event
+    // hand-offs between the streams, not the transfer, cost the step (profiles/r02_comm_modes.md).
+    static const int mode = [] { const char* e = getenv("L3_COMM_MODE"); return e ? atoi(e) : 1; }();
+    hipStream_t s = mode == 1 ? c->stream : c->comm_stream;
+    hipStream_t self_s = mode == 0 ? s : c->stream;
+    if (mode != 1) {
+        HIP_TRY(hipEventRecord(c->comm_fwd_ev, c->stream));
+        HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->comm_fwd_ev, 0));
+    }
     // RCCL has no native gather: root posts one recv per peer, peers one send, all in one
     // group so the point-to-point transfers run concurrently over the xGMI links.
     NCCL_TRY(ncclGroupStart());
@@ -1205,7 +1213,7 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
             if (r == root) {
                 if (n && dst_dev + off * VS != src_dev) {
                     const hipError_t e = hipMemcpyAsync(dst_dev + off * VS, src_dev, n * 4,
-                                                        hipMemcpyDeviceToDevice, s);
+                                                        hipMemcpyDeviceToDevice, self_s);
                     if (e != hipSuccess) {
                         (void)ncclGroupEnd();  // close the group before reporting
                         return fail("gather root copy: %s", hipGetErrorString(e));
@@ -1220,8 +1228,10 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
         NCCL_TRY(ncclSend(src_dev, (size_t)(rows_per_rank[c->rank] * VS), ncclFloat32, root, c->comm, s));
     }
     NCCL_TRY(ncclGroupEnd());
-    HIP_TRY(hipEventRecord(c->comm_done_ev, s));
-    c->gather_pending = true;
+    if (mode != 1) {
+        HIP_TRY(hipEventRecord(c->comm_done_ev, s));
+        c->gather_pending = true;
+    }
     return 0;
 }
 

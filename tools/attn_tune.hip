@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../llama3.np_amd/csrc/attn_kernel.h"
+#include "../llama3.np_amd/csrc/attn_ring.h"
 
 using namespace l3;
 
@@ -40,6 +41,19 @@ struct Variant {
                 constexpr int QW = 16 * QBW * (4 / G);                                        \
                 dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
                 hipLaunchKernelGGL((attn_fwd_v2_kernel<HD, QBW, G, KT, WPE>), grid, dim3(256), 0, s, a); \
+            }}
+
+#define AABL(ABL)                                                                             \
+    Variant{"v1<48,q4,kt64> abl" #ABL, [](const AttnArgs& a, hipStream_t s) {                  \
+                dim3 grid((a.L + 255) / 256, a.H, a.B);                                        \
+                hipLaunchKernelGGL((attn_fwd_kernel<48, 4, 1, 64, ABL>), grid, dim3(256), 0, s, a); \
+            }}
+
+#define AVAR3(QBW, KT, NS, WPE)                                                               \
+    Variant{"ring<q" #QBW ",kt" #KT ",ns" #NS ",w" #WPE ">", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * 4;                                              \
+                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
+                hipLaunchKernelGGL((attn_ring_kernel<QBW, KT, NS, WPE>), grid, dim3(256), 0, s, a); \
             }}
 
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
@@ -105,6 +119,31 @@ int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
     if (argc > 3 && std::string(argv[3]) == "c3") {  // the product C3 kernel alone (PMC passes)
         run("stories15M C3", 256, 256, 6, 6, 48, {AVAR(48, 4, 1, 64)}, rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "pf2") {
+        run("stories15M C3", 256, 256, 6, 6, 48, {AVAR(48, 4, 1, 64), AABL(32)}, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, {AVAR(48, 4, 1, 64), AABL(32)}, 1, 1, 37);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "ring") {  // LDS-DMA ring variants against v1
+        run("stories15M C3", 256, 256, 6, 6, 48,
+            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 2, 2), AVAR3(4, 64, 3, 2), AVAR3(4, 64, 2, 3),
+             AVAR3(4, 32, 2, 3), AVAR3(4, 32, 3, 3), AVAR3(4, 32, 3, 2)},
+            rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48,
+            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 2, 2), AVAR3(4, 64, 3, 2), AVAR3(4, 32, 3, 3)}, 1, 1, 37);
+        run("stories15M L=100", 16, 100, 6, 6, 48,
+            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 2, 2), AVAR3(4, 64, 3, 2), AVAR3(4, 32, 3, 3)}, 1, 1);
+        run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48,
+            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 3, 2)}, 1, 1, 19);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "abl") {  // ablations of v1 (timing only)
+        run("stories15M C3 ablations", 256, 256, 6, 6, 48,
+            {AVAR(48, 4, 1, 64), AABL(32), AABL(1), AABL(2), AABL(4), AABL(8), AABL(16), AABL(18), AABL(12),
+             AABL(1 | 8), AABL(1 | 4 | 8), AABL(1 | 4 | 8 | 16)},
+            rounds, iters);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "v2") {  // v2 (per-key-group chains) against v1

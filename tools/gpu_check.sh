@@ -35,6 +35,9 @@ for s in "$@"; do
     stamps) step stamps 300 tools/gemm_tune 1 1 stamps ;;
     attntune) step attntune 600 tools/attn_tune ;;
     attnv2) step attnv2 300 tools/attn_tune 5 10 v2 ;;
+    attnabl) step attnabl 300 tools/attn_tune 5 10 abl ;;
+    attnpf2) step attnpf2 300 tools/attn_tune 5 10 pf2 ;;
+    attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
     decode) step decode 300 python tools/bench_decode.py ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
@@ -47,6 +50,12 @@ for s in "$@"; do
     torchrun1n) step torchrun1n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     torchrun1r) step torchrun1r 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29520 bench.py --gpus 1 --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
     benchr) step benchr 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
+    benchrp0) L3_COMM_PRIORITY=0 step benchrp0 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
+    benchrng) step benchrng 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl --no-step-gather ;;
+    benchrq8) GPU_MAX_HW_QUEUES=8 step benchrq8 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
+    benchrm1) L3_COMM_MODE=1 step benchrm1 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
+    benchrm2) L3_COMM_MODE=2 step benchrm2 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
+    benchq8) GPU_MAX_HW_QUEUES=8 step benchq8 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     pmcattn) step pmcattnA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcattnA -o run --output-format csv -- tools/attn_tune 1 2 c3
            step pmcattnB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcattnB -o run --output-format csv -- tools/attn_tune 1 2 c3 ;;
     attnprof) step attnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attnprof -o run --output-format csv -- tools/attn_tune 3 10 ;;
