@@ -1,4 +1,6 @@
 // Causal attention, HD = 48 (stories15M), K/V staged by LDS-DMA into an NS-slot ring.
+// MEASURED AND REJECTED (tools/attn_tune ring): 76-78 TF/s against the
+// product kernel's 81.6 on the same box; kept for the tuner only, not part of libllama3hip.
 //
 // Same math, work split and fragment maps as attn_fwd_kernel (attn_kernel.h: "q on the lane",
 // online softmax, zig-zag q-blocks, masked body on the diagonal tile only) — replaces
@@ -17,7 +19,7 @@
 #pragma once
 #include <type_traits>
 
-#include "kernels.h"
+#include "../llama3.np_amd/csrc/kernels.h"
 
 namespace l3 {
 

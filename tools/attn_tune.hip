@@ -11,7 +11,8 @@
 #include <vector>
 
 #include "../llama3.np_amd/csrc/attn_kernel.h"
-#include "../llama3.np_amd/csrc/attn_ring.h"
+#include "attn_ring.h"
+#include "attn_variants.h"
 
 using namespace l3;
 
