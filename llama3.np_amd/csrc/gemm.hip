@@ -31,6 +31,11 @@ static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
 // lanes per unit from K: ~5-8 float4 per lane per W row in one chunk at the stories15M sizes
 template <int EPI, int MR>
 static hipError_t launch_gemv_mr(const GemmArgs& a, hipStream_t s) {
+    // L3_GEMV_LPU=16/32/64 forces the lanes per unit (A/B tuning of the decode GEMVs)
+    static const int force = [] { const char* e = getenv("L3_GEMV_LPU"); return e ? atoi(e) : 0; }();
+    if (force == 16) return launch_gemv_lpu<EPI, MR, 16>(a, s);
+    if (force == 32) return launch_gemv_lpu<EPI, MR, 32>(a, s);
+    if (force == 64) return launch_gemv_lpu<EPI, MR, 64>(a, s);
     const int k4 = a.K / 4;
     if (k4 <= 128) return launch_gemv_lpu<EPI, MR, 16>(a, s);
     if (k4 <= 256) return launch_gemv_lpu<EPI, MR, 32>(a, s);

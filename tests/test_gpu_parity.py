@@ -248,15 +248,17 @@ def test_full_size_batch_rows_independent_and_match_oracle(tmpdir_mod):
     ids = np.random.default_rng(1).integers(0, args.vocab_size, (256, 256))
     full = m(ids, 0)
     assert np.isfinite(full).all()
-    ref = orc.OracleModel(w, synth.stories15m(1))
+    m1 = llama3.Llama(path, synth.stories15m(1))
     for r in (0, 131, 255):
-        m1 = llama3.Llama(path, synth.stories15m(1))
         alone = m1(ids[r:r + 1], 0)
         # same layers bit-for-bit; only the final projection's reduction order differs
         # (B = 1 runs the lm_head through the skinny GEMV path): fp32 rounding, 1e-5 bar
         np.testing.assert_allclose(full[r:r + 1], alone, rtol=0, atol=1e-5)
-        ref = orc.OracleModel(w, synth.stories15m(1))
-        assert _close(full[r:r + 1], ref(ids[r:r + 1], 0)) <= 1e-4
+    # 16 spread rows (both batch-split halves, every 16-row block of the first and last
+    # lm_head tiles' edges) against the oracle in one batched call
+    rows = [0, 1, 15, 16, 63, 64, 100, 127, 128, 129, 131, 191, 200, 239, 254, 255]
+    ref = orc.OracleModel(w, synth.stories15m(len(rows)))
+    assert _close(full[rows], ref(ids[rows], 0)) <= 1e-4
 
 
 @pytest.mark.parametrize("B", [63, 160])

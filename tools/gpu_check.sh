@@ -40,6 +40,9 @@ for s in "$@"; do
     attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
     decode) step decode 300 python tools/bench_decode.py ;;
+    decode32) L3_GEMV_LPU=32 step decode32 300 python tools/bench_decode.py ;;
+    decode64) L3_GEMV_LPU=64 step decode64 300 python tools/bench_decode.py ;;
+    decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
     c5small) step c5small 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
