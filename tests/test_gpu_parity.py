@@ -488,6 +488,30 @@ def test_cli_end_to_end_on_synthetic_vocab(tmpdir_mod, capsys):
     assert out.startswith("\nI have a dream" + text + "\n\nToken count:"), out[:300]
 
 
+def test_cli_real_vocab_matches_reference_cli(tmpdir_mod, capsys):
+    """The reference CLI (llama3.py:324-349) with its REAL vocabulary: this package's CLI
+    prints exactly the text the reference's CLI printed on the same synthetic weights
+    (tests/golden/cli_dream.json, made by running the reference: make_cli_golden.py) — the
+    greedy ids on the GPU, the per-token decode with the reference's .strip("<s>") character
+    strip, the EOS/BOS stop rule — and the same token count."""
+    import json
+
+    from conftest import GOLDEN
+
+    with open(os.path.join(GOLDEN, "cli_dream.json"), encoding="utf-8") as f:
+        g = json.load(f)
+    args = synth.stories15m(1)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, int(g["seed"]), str(g["preset"]))
+    assert synth.digest(w) == g["weights_sha256"]
+    capsys.readouterr()
+    llama3.main([g["prompt"]], tokenizer_path=os.path.join(GOLDEN, "tokenizer.model.np"),
+                model_path=path)
+    out = capsys.readouterr().out
+    text, tail = out.split("\n\nToken count: ", 1)
+    assert text == g["stdout_before_counter"]
+    assert int(tail.split(",", 1)[0]) == g["token_count"]
+
+
 def test_cache_edges_full_context_single_token_prompt(tmpdir_mod):
     """Edges of the KV cache vs the live oracle on the GQA tiny model at B = max_batch_size:
     a one-token prompt (L = 1 at position 0: the decode attention with one key), a chunk that

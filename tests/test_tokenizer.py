@@ -1,9 +1,9 @@
 """Host tokenizer parity against the reference's own outputs (CPU).
 
 Fixture: tests/golden/tokenizer.json, produced by the reference Tokenizer.
-The vocabulary file itself is the reference's data file; it is read from
-/root/reference when present (build container) and the test is skipped
-elsewhere (the GPU box has no /root/reference).
+The vocabulary is the reference's own data file, committed as
+tests/golden/tokenizer.model.np (tests/golden/make_cli_golden.py copies it), so
+the tests run anywhere, the GPU box included.
 """
 
 import json
@@ -11,11 +11,11 @@ import os
 
 import pytest
 
-from conftest import GOLDEN, REFERENCE
+from conftest import GOLDEN
 from tokenizer import Tokenizer
 
-VOCAB = os.path.join(REFERENCE, "tokenizer.model.np")
-needs_vocab = pytest.mark.skipif(not os.path.exists(VOCAB), reason="reference vocab file absent")
+VOCAB = os.path.join(GOLDEN, "tokenizer.model.np")
+needs_vocab = pytest.mark.skipif(not os.path.exists(VOCAB), reason="vocab fixture absent")
 
 
 @pytest.fixture(scope="module")
