@@ -24,7 +24,7 @@ static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
     const int per_block = 4 * (64 / LPU);
     const dim3 grid((unsigned)((units + per_block - 1) / per_block), (unsigned)((a.M + MR - 1) / MR)),
         block(256);
-    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU>), grid, block, (size_t)MR * a.K * 4, s, a);
+    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU>), grid, block, MR == 1 ? 0 : (size_t)MR * a.K * 4, s, a);
     return hipGetLastError();
 }
 

@@ -489,7 +489,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
         wrow[0] = u;
     }
     const f32x4* W4 = reinterpret_cast<const f32x4*>(p.W);
+    // row block: rows [m0, m0 + Mb) of A (grid.y row blocks of MR rows re-read W through L2)
+    const int m0 = blockIdx.y * MR, Mb = min(MR, p.M - m0);
+    // MR == 1 (batch-1 decode): each lane loads its own float4s of the input row next to its W
+    // pieces — one memory round trip, no LDS staging pass and no block barrier; MR > 1 stages
+    // the rows once in LDS (re-read by every unit of the block)
+    constexpr bool DIRECT = MR == 1;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(a_row(p, m0));
     f32x4 w[ROWS][CH];
+    f32x4 xv[DIRECT ? CH : 1];
     auto load_chunk = [&](int t0) {
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
@@ -497,10 +505,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
 #pragma unroll
             for (int r = 0; r < ROWS; ++r)
                 w[r][t] = k4 < K4 ? W4[(int64_t)wrow[r] * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (DIRECT) xv[t] = X4[min(k4, K4 - 1)];
         }
     };
-    // row block: rows [m0, m0 + Mb) of A (grid.y row blocks of MR rows re-read W through L2)
-    const int m0 = blockIdx.y * MR, Mb = min(MR, p.M - m0);
     load_chunk(0);  // in flight while the input rows are staged
     // the epilogue's own operands (EPI_RESID: the residual; EPI_QKV: the RoPE cos / sin of the
     // pair) do not depend on the dot products: fetch them now, not after the reduction (one
@@ -537,19 +544,21 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     // stage the row block (rows past Mb zero: branch-free FMA loop), SU loads in flight per
     // thread before the first LDS store (a serial load -> store walk costs a round trip each)
     constexpr int SU = 8;
-    for (int f0 = tid; f0 < MR * K4; f0 += 256 * SU) {
-        f32x4 v[SU];
+    if constexpr (!DIRECT) {
+        for (int f0 = tid; f0 < MR * K4; f0 += 256 * SU) {
+            f32x4 v[SU];
 #pragma unroll
-        for (int u = 0; u < SU; ++u) {
-            const int f = f0 + 256 * u, m = f / K4, k4 = f - m * K4;
-            v[u] = (f < MR * K4 && m < Mb) ? reinterpret_cast<const f32x4*>(a_row(p, m0 + m))[k4]
-                                           : f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int u = 0; u < SU; ++u) {
+                const int f = f0 + 256 * u, m = f / K4, k4 = f - m * K4;
+                v[u] = (f < MR * K4 && m < Mb) ? reinterpret_cast<const f32x4*>(a_row(p, m0 + m))[k4]
+                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < SU; ++u)
+                if (f0 + 256 * u < MR * K4) reinterpret_cast<f32x4*>(xs)[f0 + 256 * u] = v[u];
         }
-#pragma unroll
-        for (int u = 0; u < SU; ++u)
-            if (f0 + 256 * u < MR * K4) reinterpret_cast<f32x4*>(xs)[f0 + 256 * u] = v[u];
+        __syncthreads();
     }
-    __syncthreads();
 
     float acc[ROWS][MR], ss[MR];
 #pragma unroll
@@ -568,8 +577,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             const int k4 = j + LPU * (t0 + t), kk = min(k4, K4 - 1);
             const float in = k4 < K4 ? 1.f : 0.f;
             f32x4 x[MR];
+            if constexpr (DIRECT) {
+                x[0] = xv[t];
+            } else {
 #pragma unroll
-            for (int m = 0; m < MR; ++m) x[m] = reinterpret_cast<const f32x4*>(xs + m * p.K)[kk];
+                for (int m = 0; m < MR; ++m) x[m] = reinterpret_cast<const f32x4*>(xs + m * p.K)[kk];
+            }
 #pragma unroll
             for (int m = 0; m < MR; ++m) {
                 ss[m] += in * (x[m].x * x[m].x + x[m].y * x[m].y + x[m].z * x[m].z + x[m].w * x[m].w);

@@ -107,10 +107,17 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
                 // before the atomic), so none sees the advanced value.
                 const int pos = st->pos, q = pos - st->hist_base;
                 if (st->hist && q >= 0 && q < st->hist_cap) st->hist[(int64_t)q * gridDim.x + blockIdx.x] = bi;
-                __threadfence();
-                if (atomicAdd(&st->arrive, 1u) == gridDim.x - 1) {
-                    st->arrive = 0u;
+                if (gridDim.x == 1) {
+                    // one row (batch-1 decode): this thread is the only reader of pos in this
+                    // launch, so it advances it directly — no agent-scope fence (≈1-3 µs of the
+                    // step) and no arrival count
                     st->pos = pos + 1;
+                } else {
+                    __threadfence();
+                    if (atomicAdd(&st->arrive, 1u) == gridDim.x - 1) {
+                        st->arrive = 0u;
+                        st->pos = pos + 1;
+                    }
                 }
             }
         }
