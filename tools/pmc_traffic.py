@@ -1,6 +1,9 @@
 """HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/pmc_gateup.json
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/pmc_gateup.json <source_hash>
+
+<source_hash> is `l3_source_hash()` of the library the passes ran (printed in every bench
+line as lib.source_hash); bench.py reports `traffic` only while the library it loads has it.
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports exactly half of the
 bytes of a wide coalesced streaming read (TCC_EA0_RDREQ x 64 B for 128-B requests), so reads
@@ -47,7 +50,7 @@ def main():
                      "python bench.py --steps 2 --warmup 1 --split 1 (every launch full size)",
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count)",
            "workload_rows": ROWS,
-           "lib_version": sys.argv[4] if len(sys.argv) > 4 else None,
+           "source_hash": sys.argv[4],
            "gateup_kernel": gu[0] if gu else None,
            "hbm_bytes_per_launch": kernels[gu[0]]["hbm_bytes_per_launch"] if gu else None,
            "algorithmic_bytes_per_launch": algo,
