@@ -136,6 +136,12 @@ struct l3_ctx {
     hipGraph_t dec_graph = nullptr;
     hipGraphExec_t dec_exec = nullptr;
     int dec_B = 0;                   // batch the graph was captured for
+    // the device loop (generate_all) replays dec_n steps per graph launch: one captured graph of
+    // dec_n consecutive decode steps (the position and ids live on the device, so the steps
+    // chain inside the graph), which removes the gap between graph launches
+    hipGraph_t dec_graph_n = nullptr;
+    hipGraphExec_t dec_exec_n = nullptr;
+    int dec_n = 0, dec_n_B = 0;
     int64_t dec_pos_mirror = -1;     // host copy of *dec_pos; -1 = device decode state invalid
     std::vector<int64_t> dec_last;   // ids the device state holds (last returned)
     int64_t graph_steps = 0;         // decode steps served by graph replay (stats)
@@ -201,6 +207,11 @@ static void drop_decode_graph(l3_ctx* c) {
     c->dec_exec = nullptr;
     c->dec_graph = nullptr;
     c->dec_B = 0;
+    if (c->dec_exec_n) (void)hipGraphExecDestroy(c->dec_exec_n);
+    if (c->dec_graph_n) (void)hipGraphDestroy(c->dec_graph_n);
+    c->dec_exec_n = nullptr;
+    c->dec_graph_n = nullptr;
+    c->dec_n = c->dec_n_B = 0;
 }
 
 static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
@@ -722,28 +733,48 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
     return 0;
 }
 
-// Capture one decode step (B sequences, L = 1) reading its position from dec_pos and its ids
-// from dec_ids; the argmax writes the next ids back into dec_ids and advances dec_pos.
-static int capture_decode_graph(l3_ctx* c, int B) {
-    drop_decode_graph(c);
+// Capture `steps` consecutive decode steps (B sequences, L = 1), each reading its position from
+// dec_pos and its ids from dec_ids; each step's argmax writes the next ids back into dec_ids and
+// advances dec_pos, so the steps chain on the device.
+static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGraphExec_t* exec) {
     const bool timing = c->timing;
     c->timing = false;  // no event records inside the graph
     HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    int rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
-    if (!rc) {
-        hipError_t e = launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, c->dec_state);
-        if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
+    int rc = 0;
+    for (int i = 0; i < steps && !rc; ++i) {
+        rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
+        if (!rc) {
+            hipError_t e = launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, c->dec_state);
+            if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
+        }
     }
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     c->timing = timing;
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
     if (e != hipSuccess) return fail("hipStreamEndCapture failed: %s", hipGetErrorString(e));
-    e = hipGraphInstantiate(&c->dec_exec, g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
     if (e != hipSuccess) { (void)hipGraphDestroy(g); return fail("hipGraphInstantiate failed: %s", hipGetErrorString(e)); }
-    c->dec_graph = g;
+    *graph = g;
+    return 0;
+}
+
+static int capture_decode_graph(l3_ctx* c, int B) {
+    drop_decode_graph(c);
+    if (capture_steps(c, B, 1, &c->dec_graph, &c->dec_exec)) return 1;
     c->dec_B = B;
     return 0;
+}
+
+// steps per graph launch in the device loop: L3_DECODE_GRAPH_STEPS (default 8; 1 = one replay
+// of the single-step graph per token)
+static int decode_graph_steps() {
+    static const int n = [] {
+        const char* e = getenv("L3_DECODE_GRAPH_STEPS");
+        const int v = e ? atoi(e) : 8;
+        return v < 1 ? 1 : v > 64 ? 64 : v;
+    }();
+    return n;
 }
 
 extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
@@ -850,10 +881,24 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
     // the graph replays only from the state the eager step above armed (position L + 2)
     if (steps > 2 && (!c->dec_exec || c->dec_B != B || c->dec_pos_mirror != L + 2))
         return done(fail("generate: decode graph not armed"));
-    for (int i = 2; i < steps; ++i) {
-        if (hipGraphLaunch(c->dec_exec, c->stream) != hipSuccess)
+    // the remaining steps - 2 steps: whole dec_n-step graphs, then single-step replays
+    const int n = decode_graph_steps();
+    if (n > 1 && steps - 2 >= n && (c->dec_n != n || c->dec_n_B != B)) {
+        if (c->dec_exec_n) (void)hipGraphExecDestroy(c->dec_exec_n);
+        if (c->dec_graph_n) (void)hipGraphDestroy(c->dec_graph_n);
+        c->dec_exec_n = nullptr;
+        c->dec_graph_n = nullptr;
+        c->dec_n = c->dec_n_B = 0;
+        if (capture_steps(c, B, n, &c->dec_graph_n, &c->dec_exec_n)) return done(1);
+        c->dec_n = n;
+        c->dec_n_B = B;
+    }
+    for (int i = 2; i < steps;) {
+        const bool multi = n > 1 && steps - i >= n;
+        if (hipGraphLaunch(multi ? c->dec_exec_n : c->dec_exec, c->stream) != hipSuccess)
             return done(fail("generate: graph replay failed"));
-        c->graph_steps++;
+        i += multi ? n : 1;
+        c->graph_steps += multi ? n : 1;
     }
     std::vector<int32_t> all((size_t)steps * B);
     if (hipMemcpyAsync(all.data(), hist, all.size() * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||

@@ -43,6 +43,10 @@ for s in "$@"; do
     decode) step decode 300 python tools/bench_decode.py ;;
     decode32) L3_GEMV_LPU=32 step decode32 300 python tools/bench_decode.py ;;
     decode64) L3_GEMV_LPU=64 step decode64 300 python tools/bench_decode.py ;;
+    decgs1) L3_DECODE_GRAPH_STEPS=1 step decgs1 300 python tools/bench_decode.py ;;
+    decgs4) L3_DECODE_GRAPH_STEPS=4 step decgs4 300 python tools/bench_decode.py ;;
+    decgs16) L3_DECODE_GRAPH_STEPS=16 step decgs16 300 python tools/bench_decode.py ;;
+    decgs32) L3_DECODE_GRAPH_STEPS=32 step decgs32 300 python tools/bench_decode.py ;;
     decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
