@@ -33,13 +33,19 @@ template <int HD>
 static hipError_t launch_decode(const AttnArgs& a, hipStream_t s) {
     constexpr int R = 256 / (HD / 4);
     const size_t lds = ((size_t)R * HD + a.Smax) * 4;
-    hipLaunchKernelGGL((attn_decode_kernel<HD>), dim3(a.H, a.B), dim3(256), lds, s, a);
+    if (a.wo) {  // O-proj fused: 64 output rows per block along z
+        if (!a.parts || a.D <= 0 || a.D % 4) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((attn_decode_kernel<HD, true>), dim3(a.H, a.B, (a.D + 63) / 64), dim3(256), lds, s, a);
+    } else {
+        hipLaunchKernelGGL((attn_decode_kernel<HD, false>), dim3(a.H, a.B), dim3(256), lds, s, a);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (a.B <= 0 || a.L <= 0) return hipSuccess;
     if (a.KVH <= 0 || a.H % a.KVH != 0) return hipErrorInvalidValue;
+    if (a.wo && (a.L != 1 || a.Smax > 8192)) return hipErrorInvalidValue;  // fused O-proj: decode only
     if (a.L == 1 && a.Smax <= 8192) {  // decode: one query per (b, h)
         switch (a.HD) {
             case 16: return launch_decode<16>(a, s);

@@ -265,9 +265,18 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
 // LDS; (2) block max and exp2 / sum; (3) P.V with rg = tid / (HD/4) key groups x HD/4 float4
 // columns, the first VP rows of each thread's V prefetched at kernel entry so their latency
 // hides under passes 1-2; partial O reduced through LDS.  q is pre-scaled by log2(e)/sqrt(HD).
-template <int HD>
+//
+// FUSE_O (decode, small D): the launch also does this head's share of the O-proj (llama3.py:211)
+// — blockIdx.z picks 64 of the D output rows, 4 lanes per row each holding a quarter of the
+// row's HD-wide Wo slice (fetched at kernel entry, beside the V prefetch) — and writes
+// parts[b][h][row] = Wo[row, h*HD:(h+1)*HD] . out[b][h].  The z blocks of one (b, h) recompute
+// the same attention (its K/V reads are small at these sizes) instead of handing it on: the
+// partial rows go to the next kernels, which add them in head order (GemmArgs::parts), so no
+// cross-block hand-off (and no agent-scope fence) is needed inside this launch.
+template <int HD, bool FUSE_O = false>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
     constexpr int D4 = HD / 4, R = 256 / D4, VP = 8;
+    constexpr int WQ = HD / 16;  // FUSE_O: float4 of the Wo row slice per lane
     extern __shared__ __attribute__((aligned(16))) float dsm[];  // [R][HD] partials, [Smax] scores
     float* red = dsm;
     float* sc = dsm + R * HD;
@@ -286,6 +295,14 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
     for (int t = 0; t < VP; ++t) {
         const int k = rg + t * R;
         vpre[t] = (rg < R && k < S) ? V4[(int64_t)k * D4 + d4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int orow = blockIdx.z * 64 + (tid >> 2), opart = tid & 3;
+    f32x4 wpre[FUSE_O ? WQ : 1];
+    if constexpr (FUSE_O) {
+        const bool ok = orow < p.D;
+        const f32x4* w4 = reinterpret_cast<const f32x4*>(p.wo + (int64_t)(ok ? orow : 0) * (p.H * HD) + h * HD) + opart * WQ;
+#pragma unroll
+        for (int i = 0; i < WQ; ++i) wpre[i] = ok ? w4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
     const f32x4* q4 = reinterpret_cast<const f32x4*>(p.q + ((int64_t)b * p.H + h) * HD);
     f32x4 q[D4];
@@ -331,10 +348,24 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
         reinterpret_cast<f32x4*>(red)[rg * D4 + d4] = acc;
     }
     __syncthreads();
+    __shared__ f32x4 oh[D4];
     if (tid < D4) {
         f32x4 o = {0.f, 0.f, 0.f, 0.f};
         for (int r = 0; r < R; ++r) o += reinterpret_cast<const f32x4*>(red)[r * D4 + tid];
-        reinterpret_cast<f32x4*>(p.out + ((int64_t)b * p.H + h) * HD)[tid] = o * (1.0f / l);
+        if constexpr (FUSE_O) oh[tid] = o * (1.0f / l);
+        else reinterpret_cast<f32x4*>(p.out + ((int64_t)b * p.H + h) * HD)[tid] = o * (1.0f / l);
+    }
+    if constexpr (FUSE_O) {
+        __syncthreads();
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < WQ; ++i) {
+            const f32x4 ov = oh[opart * WQ + i];
+            acc += wpre[i].x * ov.x + wpre[i].y * ov.y + wpre[i].z * ov.z + wpre[i].w * ov.w;
+        }
+        acc += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc), 0xB1, 0xF, 0xF, false));
+        acc += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(acc), 0x4E, 0xF, 0xF, false));
+        if (opart == 0 && orow < p.D) p.parts[((int64_t)b * p.H + h) * p.D + orow] = acc;
     }
 }
 

@@ -18,14 +18,30 @@ static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int EPI, int MR, int LPU>
+template <int EPI, int MR, int LPU, bool PARTS = false>
 static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
     const int units = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? a.N / 2 : a.N;
     const int per_block = 4 * (64 / LPU);
     const dim3 grid((unsigned)((units + per_block - 1) / per_block), (unsigned)((a.M + MR - 1) / MR)),
         block(256);
-    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU>), grid, block, MR == 1 ? 0 : (size_t)MR * a.K * 4, s, a);
+    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU, PARTS>), grid, block, MR == 1 ? 0 : (size_t)MR * a.K * 4, s, a);
     return hipGetLastError();
+}
+
+// the O-proj partial rows of the fused decode attention (GemmArgs::parts): EPI_SWIGLU carries
+// GEMV_MAXP partial loads per piece, so its lanes take fewer pieces (<= 4 up to K = 1024)
+template <int EPI>
+static hipError_t launch_gemv_parts(const GemmArgs& a, hipStream_t s) {
+    if (a.nparts < 1 || a.nparts > GEMV_MAXP || !gemv_direct(a)) return hipErrorInvalidValue;
+    const int k4 = a.K / 4;
+    if constexpr (EPI == EPI_SWIGLU) {
+        if (k4 <= 128) return launch_gemv_lpu<EPI, 1, 32, true>(a, s);
+        return launch_gemv_lpu<EPI, 1, 64, true>(a, s);
+    } else {
+        if (k4 <= 128) return launch_gemv_lpu<EPI, 1, 16, true>(a, s);
+        if (k4 <= 256) return launch_gemv_lpu<EPI, 1, 32, true>(a, s);
+        return launch_gemv_lpu<EPI, 1, 64, true>(a, s);
+    }
 }
 
 // lanes per unit from K: ~5-8 float4 per lane per W row in one chunk at the stories15M sizes
@@ -56,6 +72,12 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
     return launch_gemv_mr<EPI, 8>(a, s);
 }
 
+bool gemv_direct(const GemmArgs& a) {
+    static const int cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 8; }();
+    const bool small_w = (int64_t)a.N * a.K <= (int64_t)4 << 20;
+    return gemm_is_gemv(a) && (a.M <= 1 || cap == 1 || (small_w && a.M <= 8));
+}
+
 bool gemm_is_gemv(const GemmArgs& a) {
     const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
     const bool short_m = a.M <= 8 || (a.M <= 256 && (int64_t)a.N * a.K <= (int64_t)4 << 20);
@@ -78,6 +100,13 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     // epilogues, 8-row blocks beyond M = 8 re-reading W through L2 — for the layer weights up
     // to M = 256 (a 128-row MFMA tile there is one k-loop of memory round trips on a handful of
     // blocks); the 37 MB lm_head keeps the MFMA tiles past M = 8
+    if (a.parts) {
+        switch (epi) {
+            case EPI_SWIGLU: return launch_gemv_parts<EPI_SWIGLU>(a, s);
+            case EPI_RESID: return launch_gemv_parts<EPI_RESID>(a, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (gemm_is_gemv(a)) {
         switch (epi) {
             case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);

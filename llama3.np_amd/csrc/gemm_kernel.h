@@ -465,12 +465,20 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 // load), and a butterfly over the LPU lanes completes the dot products.  The M input rows are
 // staged in LDS once per block; the RMSNorm sum of squares comes from the same lane-split reads
 // (the norm weight itself is folded into W, launch_fold_cols).
-template <int EPI, int MR, int LPU>
+//
+// PARTS (decode with the O-proj fused into attention, MR = 1 only): p.parts holds the per-head
+// O-proj rows [M][nparts][D]; EPI_SWIGLU adds them to its input row (h + attention . Wo^T, the
+// FFN's input, llama3.py:253), EPI_RESID to its residual (the down-proj's residual is that same
+// row, :259), always in head order.  Their loads join the same round trip (GEMV_MAXP per
+// piece, predicated past nparts, so CH drops to 4).
+template <int EPI, int MR, int LPU, bool PARTS = false>
 __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     extern __shared__ __attribute__((aligned(16))) float xs[];  // [MR][K]
+    static_assert(!PARTS || MR == 1, "partial rows only on the one-row GEMV");
     constexpr int ROWS = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? 2 : 1;
     constexpr int UPW = 64 / LPU;  // units per wave
-    constexpr int CH = 8;          // float4 per W row per lane in flight
+    constexpr int CH = PARTS ? 4 : 8;  // float4 per W row per lane in flight
+    constexpr bool XPARTS = PARTS && EPI == EPI_SWIGLU;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int K4 = p.K >> 2;
     const int j = lane % LPU;
@@ -498,6 +506,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     const f32x4* X4 = reinterpret_cast<const f32x4*>(a_row(p, m0));
     f32x4 w[ROWS][CH];
     f32x4 xv[DIRECT ? CH : 1];
+    f32x4 xp[XPARTS ? CH : 1][XPARTS ? GEMV_MAXP : 1];
+    const f32x4* P4 = reinterpret_cast<const f32x4*>(p.parts) + (int64_t)m0 * p.nparts * K4;
     auto load_chunk = [&](int t0) {
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
@@ -506,6 +516,20 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             for (int r = 0; r < ROWS; ++r)
                 w[r][t] = k4 < K4 ? W4[(int64_t)wrow[r] * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
             if constexpr (DIRECT) xv[t] = X4[min(k4, K4 - 1)];
+            if constexpr (XPARTS) {
+#pragma unroll
+                for (int pp = 0; pp < GEMV_MAXP; ++pp)
+                    xp[t][pp] = (pp < p.nparts && k4 < K4) ? P4[(int64_t)pp * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        }
+    };
+    // x = A row + the heads' O-proj rows, summed in head order
+    auto add_parts = [&]() {
+        if constexpr (XPARTS) {
+#pragma unroll
+            for (int t = 0; t < CH; ++t)
+#pragma unroll
+                for (int pp = 0; pp < GEMV_MAXP; ++pp) xv[t] += xp[t][pp];
         }
     };
     load_chunk(0);  // in flight while the input rows are staged
@@ -530,6 +554,14 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
         const int m = m0 + mi;
         if constexpr (EPI == EPI_RESID) {
             pre0[mi] = *res_at(p, m, unit);
+            if constexpr (PARTS) {
+                float pr[GEMV_MAXP];
+#pragma unroll
+                for (int pp = 0; pp < GEMV_MAXP; ++pp)
+                    pr[pp] = pp < p.nparts ? p.parts[((int64_t)m * p.nparts + pp) * p.ldc + unit] : 0.f;
+#pragma unroll
+                for (int pp = 0; pp < GEMV_MAXP; ++pp) pre0[mi] += pr[pp];
+            }
         } else if constexpr (EPI == EPI_QKV) {
             if (qkv_sec < 2) {
                 const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
@@ -570,6 +602,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     const int nt = (K4 + LPU - 1) / LPU;
     for (int t0 = 0; t0 < nt; t0 += CH) {
         if (t0) load_chunk(t0);
+        add_parts();
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             if (t0 + t >= nt) break;  // wave-uniform

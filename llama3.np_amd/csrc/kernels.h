@@ -34,7 +34,12 @@ struct GemmArgs {
     // of reading C, so the residual stream h is first written by layer 0's O-proj
     const int32_t* a_rows;
     const float* res_src; const int32_t* res_rows;
+    // Decode with the O-proj fused into attention (attn_decode_kernel<HD, true>): the O-proj
+    // arrives as nparts (= n_heads, <= GEMV_MAXP) per-head partial rows [M][nparts][D] that the
+    // GEMV adds to its A row (EPI_SWIGLU) or to its residual (EPI_RESID) in head order
+    const float* parts; int nparts;
 };
+constexpr int GEMV_MAXP = 8;
 
 // Device-resident state of the greedy decode loop (graph replay).  pos is first, so &st->pos
 // is the pos_dev the captured kernels read.
@@ -123,6 +128,12 @@ struct AttnArgs {
     float* out;           // [B*L, H*HD]
     int B, L, start_pos, H, KVH, HD, Smax;
     const int* pos_dev;   // if set, start_pos is read from device memory (graph replay)
+    // decode only: when wo is set the launch also applies the O-proj (llama3.py:211) per head:
+    // parts[b][h][0:D] = Wo[:, h*HD:(h+1)*HD] . out[b][h] (out itself is not written); the
+    // residual add and the sum over heads happen in the consumers (GemmArgs::parts)
+    const float* wo;      // [D, H*HD]
+    float* parts;         // [B, H, D]
+    int D;
 };
 
 // start position of a launch: the argument, or the device word a captured decode graph reads
@@ -137,6 +148,9 @@ hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out,
                          DecState* st = nullptr);
 // true when launch_gemm runs this shape on the row-blocked GEMV (short M)
 bool gemm_is_gemv(const GemmArgs& a);
+// true when that GEMV runs one row per block with the input row read per lane (the only form
+// that takes GemmArgs::parts)
+bool gemv_direct(const GemmArgs& a);
 // which EPI_STORE kernel launch_gemm picks (0 = GEMV): launches of equal id round identically
 // row by row, whatever their M
 int gemm_store_config(const GemmArgs& a);

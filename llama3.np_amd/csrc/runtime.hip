@@ -106,6 +106,7 @@ struct l3_ctx {
     // workspace
     int64_t ws_T = 0, ws_B = 0;
     float *h = nullptr, *q = nullptr, *attn = nullptr, *hid = nullptr, *logits = nullptr;
+    float* oparts = nullptr;         // [8, H, D] per-head O-proj rows of the fused decode attention
     int32_t *ids = nullptr, *amax = nullptr;
     int32_t* ids_pin = nullptr;      // pinned host staging of the int32 ids (upload_ids)
     int64_t ids_pin_n = 0;
@@ -220,7 +221,8 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     drop_decode_graph(c);  // the captured graph holds workspace pointers
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits);
-    dfree(c->ids); dfree(c->amax);
+    dfree(c->ids); dfree(c->amax); dfree(c->oparts);
+    c->oparts = nullptr;
     const int64_t Tn = T > c->ws_T ? T : c->ws_T;
     const int64_t Bn = B > c->ws_B ? B : c->ws_B;
     const int64_t D = c->d.dim;
@@ -231,6 +233,8 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     HIP_TRY(hipMalloc(&c->logits, Bn * (int64_t)c->d.vocab_size * 4));
     HIP_TRY(hipMalloc(&c->ids, Tn * 4));
     HIP_TRY(hipMalloc(&c->amax, Bn * 4));
+    if (c->d.n_heads <= GEMV_MAXP && D <= 1024)
+        HIP_TRY(hipMalloc(&c->oparts, (int64_t)8 * c->d.n_heads * D * 4));
     c->ws_T = Tn;
     c->ws_B = Bn;
     return 0;
@@ -241,7 +245,7 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 11;
+    if (minor) *minor = 12;
     return 0;
 }
 
@@ -343,6 +347,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     }
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
+    dfree(c->oparts);
     dfree(c->amax); dfree(c->gather_ids);
     if (c->ids_pin) (void)hipHostFree(c->ids_pin);
     for (void* p : c->scratch) dfree(p);
@@ -546,28 +551,44 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     if (emb_ids) { g.A = c->emb; g.a_rows = emb_ids; }
     if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
+    GemmArgs gu{};  // rmsnorm -> gate|up -> SwiGLU
+    gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
+    gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true;  // n_ffn folded into wgu
+    gu.eps = c->d.norm_eps;
+    GemmArgs dn{};  // down + residual
+    dn.A = hid; dn.lda = FD; dn.W = Ly.wd; dn.C = h; dn.ldc = D;
+    dn.M = (int)T; dn.N = D; dn.K = FD; dn.norm = false;
+    // Batch-1 decode: the O-proj rides in the attention launch as per-head partial rows, which
+    // gate|up adds to its input and down to its residual (h + attn . Wo^T, llama3.py:211,253),
+    // so a step runs one launch per layer fewer (device loop 0.104 -> 0.101 ms/step; at B = 8
+    // the redundant attention of the z blocks costs more than the launch: 0.129 -> 0.134, so
+    // B > 1 keeps the O-proj GEMV).  L3_DECODE_FUSE_O=0 keeps it at B = 1 too (A/B).
+    static const bool fuse_env = [] { const char* e = getenv("L3_DECODE_FUSE_O"); return !e || e[0] != '0'; }();
+    const bool fuse_o = fuse_env && L == 1 && c->oparts && b0 == 0 && T == 1 && D % 4 == 0 && c->HD % 16 == 0 &&
+                        c->d.max_seq_len <= 8192 && gemv_direct(gu) && gemv_direct(dn);
     // causal attention over the cache
     AttnArgs a{};
     a.q = q; a.cache_k = Ly.cache_k + cache0; a.cache_v = Ly.cache_v + cache0; a.out = attn;
     a.B = B; a.L = L; a.start_pos = start_pos; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
     a.HD = c->HD; a.Smax = c->d.max_seq_len; a.pos_dev = pos_dev;
+    if (fuse_o) { a.wo = Ly.wo; a.parts = c->oparts; a.D = D; }
     if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention(a, s); })) return 1;
-    // O-proj + residual (in place on h)
-    GemmArgs o{};
-    o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.C = h; o.ldc = D;
-    o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
-    if (emb_ids) { o.res_src = c->emb; o.res_rows = emb_ids; }  // h = emb[ids] + attn . Wo^T
-    if (timed_on(c, L3_K_OPROJ, s, [&] { return launch_gemm(EPI_RESID, o, s); })) return 1;
-    // rmsnorm -> gate|up -> SwiGLU
-    GemmArgs gu{};
-    gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
-    gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true;  // n_ffn folded into wgu
-    gu.eps = c->d.norm_eps;
+    if (fuse_o) {
+        gu.parts = dn.parts = c->oparts;
+        gu.nparts = dn.nparts = c->d.n_heads;
+        if (emb_ids) {  // layer 0: the residual stream is still the embedding row
+            gu.A = c->emb; gu.a_rows = emb_ids;
+            dn.res_src = c->emb; dn.res_rows = emb_ids;
+        }
+    } else {
+        // O-proj + residual (in place on h)
+        GemmArgs o{};
+        o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.C = h; o.ldc = D;
+        o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
+        if (emb_ids) { o.res_src = c->emb; o.res_rows = emb_ids; }  // h = emb[ids] + attn . Wo^T
+        if (timed_on(c, L3_K_OPROJ, s, [&] { return launch_gemm(EPI_RESID, o, s); })) return 1;
+    }
     if (timed_on(c, L3_K_GATEUP, s, [&] { return launch_gemm(EPI_SWIGLU, gu, s); })) return 1;
-    // down + residual
-    GemmArgs dn{};
-    dn.A = hid; dn.lda = FD; dn.W = Ly.wd; dn.C = h; dn.ldc = D;
-    dn.M = (int)T; dn.N = D; dn.K = FD; dn.norm = false;
     if (timed_on(c, L3_K_DOWN, s, [&] { return launch_gemm(EPI_RESID, dn, s); })) return 1;
     return 0;
 }
