@@ -55,8 +55,8 @@ B_PER_GPU, SEQ = 256, 256
 
 class Dist:
     """One process per GPU (torchrun env).  No PyTorch in this process: the RCCL id goes
-    rank 0 -> peers through an atomically renamed file (single node, keyed by the launcher's
-    pid and MASTER_PORT), and barriers / the max-over-ranks time run over RCCL itself."""
+    rank 0 -> peers through an atomically renamed file (single node, l3hip.launch_key()), and
+    barriers / the max-over-ranks time run over RCCL itself."""
 
     def __init__(self, n, force_comm=False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -74,15 +74,12 @@ class Dist:
     def init_comm(self, ctx):
         self.ctx = ctx
         if self.world > 1 or self.force_comm:
-            key = uid_key()
+            key = l3hip.launch_key()
             uid = l3hip.exchange_unique_id(self.rank, self.world, key)
             ctx.comm_init(self.world, self.rank, uid)
             ctx.comm_barrier()
-            if self.rank == 0:  # every rank has read the id once the barrier completed
-                try:
-                    os.remove(os.path.join("/tmp", f"l3_rccl_uid_{key}"))
-                except OSError:
-                    pass
+            if self.rank == 0:  # every rank has read the id once the communicator is up
+                l3hip.remove_unique_id(key)
 
     def barrier(self):
         if self.comm:
@@ -90,14 +87,6 @@ class Dist:
 
     def max(self, x):
         return self.ctx.comm_max(x) if self.comm else x
-
-
-def uid_key():
-    """Name of the RCCL-id hand-off file, equal on every rank of one launch: torchrun's run id
-    (TORCHELASTIC_RUN_ID, shared by the ranks of one launch) or else the launcher pid, plus
-    MASTER_PORT."""
-    run = os.environ.get("TORCHELASTIC_RUN_ID") or str(os.getppid())
-    return f"{run}_{os.environ.get('MASTER_PORT', '0')}"
 
 
 def cpu_baseline():

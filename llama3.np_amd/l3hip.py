@@ -393,6 +393,24 @@ class Context:
         return y
 
 
+def launch_key() -> str:
+    """Key of the RCCL-id hand-off file: equal on every rank of one launch, different for every
+    launch — torchrun's run id (TORCHELASTIC_RUN_ID; "none" under the default static rendezvous,
+    so not unique alone), the launcher's pid (torchrun's agent is the parent of every rank it
+    starts) and MASTER_PORT."""
+    run = os.environ.get("TORCHELASTIC_RUN_ID") or "local"
+    return f"{run}_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+
+
+def remove_unique_id(key: str) -> None:
+    """Rank 0, once every rank has joined the communicator (ncclCommInitRank is collective, so
+    every rank has read the id by then): drop the hand-off file."""
+    try:
+        os.remove(os.path.join("/tmp", f"l3_rccl_uid_{key}"))
+    except OSError:
+        pass
+
+
 def exchange_unique_id(rank: int, world: int, key: str, timeout_s: float = 120.0) -> bytes:
     """Ship the 128-byte RCCL id from rank 0 to the other ranks of ONE node through an
     atomically renamed file in /tmp (no PyTorch / gloo needed).  ``key`` must be unique per

@@ -79,9 +79,7 @@ class ShardedPrefill:
                   bcast_uid: Optional[Callable[[Optional[bytes]], bytes]] = None, root: int = 0):
         """Wire to a ``llama3.Llama`` on this rank's GPU.  ``bcast_uid`` ships the
         128-byte RCCL id from the root to every rank (any host-side channel); by default a
-        file hand-off in /tmp keyed by the launcher pid and MASTER_PORT (one node)."""
-        import os
-
+        file hand-off in /tmp keyed by ``l3hip.launch_key()`` (one node)."""
         import l3hip
 
         ctx = model.context
@@ -89,11 +87,13 @@ class ShardedPrefill:
         if bcast_uid is None:
             if root != 0:
                 raise ValueError("the default id exchange needs root 0")
-            key = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
+            key = l3hip.launch_key()
             uid = l3hip.exchange_unique_id(rank, world, key)
         else:
             uid = bcast_uid(l3hip.comm_unique_id() if rank == root else None)
         ctx.comm_init(world, rank, uid)
+        if bcast_uid is None and rank == 0:
+            l3hip.remove_unique_id(key)
         bufs = {}
 
         def buffer(name, nbytes):
