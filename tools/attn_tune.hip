@@ -13,6 +13,7 @@
 #include "../llama3.np_amd/csrc/attn_kernel.h"
 #include "attn_ring.h"
 #include "attn_variants.h"
+#include "attn_v3.h"
 
 using namespace l3;
 
@@ -55,6 +56,13 @@ struct Variant {
                 constexpr int QW = 16 * QBW * 4;                                              \
                 dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
                 hipLaunchKernelGGL((attn_ring_kernel<QBW, KT, NS, WPE>), grid, dim3(256), 0, s, a); \
+            }}
+
+#define AV3(NW, QBW, KT, LZ, SD)                                                              \
+    Variant{"v3<w" #NW ",q" #QBW ",kt" #KT ",lazy" #LZ ",skip" #SD ">", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * NW;                                             \
+                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
+                hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD>), grid, dim3(64 * NW), 0, s, a); \
             }}
 
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
@@ -145,6 +153,15 @@ int main(int argc, char** argv) {
             {AVAR(48, 4, 1, 64), AABL(32), AABL(1), AABL(2), AABL(4), AABL(8), AABL(16), AABL(18), AABL(12),
              AABL(1 | 8), AABL(1 | 4 | 8), AABL(1 | 4 | 8 | 16)},
             rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "v3") {  // lazy rescale / dead-group skip / 8 waves
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AV3(4, 4, 64, false, false), AV3(4, 4, 64, true, false),
+                                  AV3(4, 4, 64, false, true), AV3(4, 4, 64, true, true),
+                                  AV3(8, 2, 64, false, false), AV3(8, 2, 64, true, true), AV3(8, 2, 32, true, true)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48, v, 1, 1, 19);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "v2") {  // v2 (per-key-group chains) against v1
