@@ -183,6 +183,10 @@ int l3_synchronize(l3_ctx* ctx);
 int l3_kernel_timing(l3_ctx* ctx, int32_t mask);
 /* total milliseconds and launch count per l3_kernel_id since last reset */
 int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
+/* Greedy-decode counters (extension; llama3.py:310-321 has no counterpart): decode steps
+ * served by a captured-graph replay, and of those the ones a speculative step (launched when
+ * the previous l3_greedy_step_host returned) answered. */
+int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits);
 
 /* ---- multi-GPU: batch-sharded prefill + RCCL logits gather (xGMI) -------- */
 /* 128-byte RCCL unique id (rank 0 creates, every rank receives it). */

@@ -538,6 +538,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     // memory round trip less per launch; decode runs three such launches per layer)
     const bool writer = j == 0 && valid;
     float pre0[MR], pre1[MR];
+    float2 bak_old[EPI == EPI_QKV ? MR : 1];
     int qkv_sec = 0, qkv_head = 0, qkv_d = 0;  // EPI_QKV: 0 q, 1 k, 2 v; head; column in head
     if constexpr (EPI == EPI_QKV) {
         const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD, col = 2 * u;
@@ -570,6 +571,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                 pre1[mi] = p.rope_sin[t];
             } else {
                 pre0[mi] = 1.f;  // V: identity rotation
+            }
+            if (p.kv_bak && qkv_sec > 0) {  // the slot's previous K / V pair (see GemmArgs::kv_bak)
+                const int bidx = m / p.L, pos = start_of(p) + m - bidx * p.L;
+                bak_old[mi] = *reinterpret_cast<const float2*>(
+                    (qkv_sec == 1 ? p.cache_k : p.cache_v) +
+                    (((int64_t)bidx * p.KVH + qkv_head) * p.Smax + pos) * p.HD + qkv_d);
             }
         }
     }
@@ -651,6 +658,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                               ? reinterpret_cast<float2*>(p.q_out + (int64_t)m * qdim + col)
                               : reinterpret_cast<float2*>((qkv_sec == 1 ? p.cache_k : p.cache_v) +
                                                           (((int64_t)bidx * p.KVH + qkv_head) * p.Smax + pos) * p.HD + qkv_d);
+            if (p.kv_bak && qkv_sec > 0)  // [pos parity][k, v][batch row][KV head][HD]
+                *reinterpret_cast<float2*>(p.kv_bak + (((((int64_t)(pos & 1) * 2 + qkv_sec - 1) * (p.M / p.L) + bidx) * p.KVH +
+                                                        qkv_head) * p.HD + qkv_d)) = bak_old[mi];
             *dst = qkv_sec == 0 ? float2{r0 * p.q_scale, r1 * p.q_scale} : float2{r0, r1};
         } else {
             float* dst = p.C + (int64_t)m * p.ldc + unit;

@@ -28,6 +28,10 @@ struct GemmArgs {
     int L, start_pos, H, KVH, HD, Smax;
     const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
+    // EPI_QKV on the GEMV (captured batch-1..8 decode step): before appending K / V at pos, keep
+    // the slot's previous contents in kv_bak [pos & 1][2: k, v][M][KVH][HD], so a speculatively
+    // run decode step (two in flight: consecutive positions) can be undone (runtime.hip)
+    float* kv_bak;
     unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 10 per block
     // Embedding fused into layer 0 (llama3.py:287): when set, A row r is A + a_rows[r] * lda
     // (the token's embedding row) and EPI_RESID adds res_src[res_rows[r] * ldc + col] instead
@@ -159,6 +163,9 @@ hipError_t launch_silu(const float* x, float* y, int64_t n, hipStream_t s);
 hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows, int dim,
                           float eps, hipStream_t s);
 hipError_t launch_fold_cols(float* W, int64_t rows, int K, const float* w, hipStream_t s);
+// cache[b][h][pos][:] = bak[b][h][:] for b < B, h < KVH (undo of a speculative decode step)
+hipError_t launch_kv_restore(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos,
+                             hipStream_t s);
 hipError_t launch_rope(const float* x, float* y, const float* cos_t, const float* sin_t, int B,
                        int L, int nh, int hd, hipStream_t s);
 

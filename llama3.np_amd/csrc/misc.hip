@@ -239,4 +239,21 @@ hipError_t launch_fold_cols(float* W, int64_t rows, int K, const float* w, hipSt
     return hipGetLastError();
 }
 
+// undo of a speculative decode step's K / V append (runtime.hip, l3_greedy_step_host)
+__global__ void kv_restore_kernel(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * KVH * HD) return;
+    const int d = i % HD, bh = i / HD;  // bh = b * KVH + h
+    cache[((int64_t)bh * Smax + pos) * HD + d] = bak[i];
+}
+
+hipError_t launch_kv_restore(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos,
+                             hipStream_t s) {
+    const int n = B * KVH * HD;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(kv_restore_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cache, bak, B, KVH,
+                       Smax, HD, pos);
+    return hipGetLastError();
+}
+
 }  // namespace l3

@@ -146,6 +146,21 @@ struct l3_ctx {
     int64_t dec_pos_mirror = -1;     // host copy of *dec_pos; -1 = device decode state invalid
     std::vector<int64_t> dec_last;   // ids the device state holds (last returned)
     int64_t graph_steps = 0;         // decode steps served by graph replay (stats)
+    // Speculative decode (lazy generate): when a step returns, the next SPEC_DEPTH steps are
+    // already queued as graph replays (the ids chain on the device), so the GPU keeps running
+    // while the host yields; each captured step keeps the K / V slot it overwrites in kv_bak
+    // (one copy per position parity), and a call that does not continue the schedule restores
+    // the slots of every step still pending
+    static constexpr int SPEC_DEPTH = 2;
+    float* kv_bak = nullptr;         // [n_layers][2 parities][2: k, v][8][KVH][HD]
+    bool bak_capture = false;        // run_layer: QKV launches keep the overwritten slot
+    bool dec_bak = false;            // the captured single-step graph keeps it
+    bool in_loop = false;            // generate_all drives the device state itself
+    int spec_n = 0, spec_B = 0;      // steps in flight (oldest first), their batch
+    int spec_pos[SPEC_DEPTH] = {0, 0};
+    int32_t* spec_host[SPEC_DEPTH] = {nullptr, nullptr};  // pinned: each step's ids
+    hipEvent_t spec_ev[SPEC_DEPTH] = {nullptr, nullptr};
+    int64_t spec_hits = 0;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -159,6 +174,8 @@ static int set_dev(l3_ctx* c, bool join = true) {
     }
     return 0;
 }
+
+static int spec_resolve(l3_ctx* c);  // undo of a speculative decode step (below)
 
 template <typename F>
 static int timed_on(l3_ctx* c, int kind, hipStream_t s, F&& launch) {
@@ -208,6 +225,7 @@ static void drop_decode_graph(l3_ctx* c) {
     c->dec_exec = nullptr;
     c->dec_graph = nullptr;
     c->dec_B = 0;
+    c->dec_bak = false;
     if (c->dec_exec_n) (void)hipGraphExecDestroy(c->dec_exec_n);
     if (c->dec_graph_n) (void)hipGraphDestroy(c->dec_graph_n);
     c->dec_exec_n = nullptr;
@@ -245,7 +263,7 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 12;
+    if (minor) *minor = 13;
     return 0;
 }
 
@@ -353,8 +371,12 @@ extern "C" int l3_destroy(l3_ctx* c) {
     for (void* p : c->scratch) dfree(p);
     for (auto& t : c->timers) { (void)hipEventDestroy(t.a); (void)hipEventDestroy(t.b); }
     drop_decode_graph(c);
-    dfree(c->dec_ids); dfree(c->dec_state);
+    dfree(c->dec_ids); dfree(c->dec_state); dfree(c->kv_bak);
     if (c->dec_host) (void)hipHostFree(c->dec_host);
+    for (int i = 0; i < l3_ctx::SPEC_DEPTH; ++i) {
+        if (c->spec_ev[i]) (void)hipEventDestroy(c->spec_ev[i]);
+        if (c->spec_host[i]) (void)hipHostFree(c->spec_host[i]);
+    }
     for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i) {
         if (c->aux[i]) { (void)hipStreamSynchronize(c->aux[i]); (void)hipStreamDestroy(c->aux[i]); }
         if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
@@ -497,6 +519,8 @@ static int need_model(l3_ctx* c) {
 extern "C" int l3_reset_cache(l3_ctx* c) {
     CHECK_CTX(c);
     if (set_dev(c)) return 1;
+    c->spec_n = 0;  // the whole cache is cleared: nothing to restore
+    c->dec_pos_mirror = -1;
     const int64_t cache = (int64_t)c->d.max_batch_size * c->d.n_kv_heads * c->d.max_seq_len * c->HD * 4;
     for (auto& L : c->layers) {
         HIP_TRY(hipMemsetAsync(L.cache_k, 0, cache, c->stream));
@@ -550,6 +574,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     g.pos_dev = pos_dev;
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     if (emb_ids) { g.A = c->emb; g.a_rows = emb_ids; }
+    if (c->bak_capture) g.kv_bak = c->kv_bak + (int64_t)li * 2 * 2 * 8 * c->d.n_kv_heads * c->HD;
     if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
     GemmArgs gu{};  // rmsnorm -> gate|up -> SwiGLU
     gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
@@ -739,7 +764,7 @@ extern "C" int l3_set_batch_split(l3_ctx* c, int32_t parts, int64_t min_tokens) 
 extern "C" int l3_forward_dev(l3_ctx* c, const int32_t* ids_dev, int32_t B, int32_t L,
                               int32_t start_pos, float* logits_dev) {
     CHECK_CTX(c);
-    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c, false) || ensure_ws(c, B, L))
+    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c, false) || spec_resolve(c) || ensure_ws(c, B, L))
         return 1;
     return forward_dev(c, ids_dev, B, L, start_pos, logits_dev);
 }
@@ -747,7 +772,8 @@ extern "C" int l3_forward_dev(l3_ctx* c, const int32_t* ids_dev, int32_t B, int3
 extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
                                int32_t start_pos, float* logits_host) {
     CHECK_CTX(c);
-    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
+    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || spec_resolve(c) || ensure_ws(c, B, L))
+        return 1;
     if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
     if (forward_dev(c, c->ids, B, L, start_pos, c->logits, nullptr, logits_host)) return 1;
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -780,10 +806,67 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
     return 0;
 }
 
+static bool speculation_on() {
+    static const bool on = [] { const char* e = getenv("L3_DECODE_SPECULATE"); return !e || e[0] != '0'; }();
+    return on;
+}
+
 static int capture_decode_graph(l3_ctx* c, int B) {
     drop_decode_graph(c);
-    if (capture_steps(c, B, 1, &c->dec_graph, &c->dec_exec)) return 1;
+    // B <= 8: every QKV of the step runs on the GEMV, whose epilogue keeps the overwritten slot
+    const bool bak = speculation_on() && B <= 8;
+    if (bak && !c->kv_bak)
+        HIP_TRY(hipMalloc(&c->kv_bak, (size_t)c->layers.size() * 2 * 2 * 8 * c->d.n_kv_heads * c->HD * 4));
+    c->bak_capture = bak;
+    const int rc = capture_steps(c, B, 1, &c->dec_graph, &c->dec_exec);
+    c->bak_capture = false;
+    if (rc) return 1;
     c->dec_B = B;
+    c->dec_bak = bak;
+    return 0;
+}
+
+// Queue captured steps until SPEC_DEPTH are in flight, each at the position after the last
+// (dec_pos_mirror is the position the device state will reach); their ids land in spec_host
+// behind spec_ev.
+static int speculate(l3_ctx* c, int B) {
+    if (!speculation_on() || c->in_loop || !c->dec_exec || !c->dec_bak || c->dec_B != B || c->timing ||
+        c->dec_pos_mirror < 0)
+        return 0;
+    while (c->spec_n < l3_ctx::SPEC_DEPTH) {
+        const int pos = (int)c->dec_pos_mirror + c->spec_n;
+        if (pos >= c->d.max_seq_len) break;
+        const int k = c->spec_n;
+        if (!c->spec_ev[k]) HIP_TRY(hipEventCreateWithFlags(&c->spec_ev[k], hipEventDisableTiming));
+        if (!c->spec_host[k]) HIP_TRY(hipHostMalloc(&c->spec_host[k], (size_t)c->d.max_batch_size * 4));
+        HIP_TRY(hipGraphLaunch(c->dec_exec, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->spec_host[k], c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipEventRecord(c->spec_ev[k], c->stream));
+        c->spec_pos[k] = pos;
+        c->spec_B = B;
+        ++c->spec_n;
+    }
+    return 0;
+}
+
+// Undo the speculative steps nobody asked for: put back the K / V slot each appended in every
+// layer (stream-ordered after them) and drop the device decode state (the next eager step
+// re-arms it).  Every entry point that reads the cache calls this first, so the cache always
+// holds what the reference's would.
+static int spec_resolve(l3_ctx* c) {
+    if (!c->spec_n) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    const int KVH = c->d.n_kv_heads, HD = c->HD, n = c->spec_B * KVH * HD;
+    for (int k = c->spec_n - 1; k >= 0; --k) {
+        const int pos = c->spec_pos[k];
+        for (size_t li = 0; li < c->layers.size(); ++li) {
+            const float* bak = c->kv_bak + (int64_t)li * 2 * 2 * 8 * KVH * HD + (int64_t)(pos & 1) * 2 * n;
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_k, bak, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
+        }
+    }
+    c->spec_n = 0;
+    c->dec_pos_mirror = -1;
     return 0;
 }
 
@@ -809,6 +892,34 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
         c->dec_pos = &c->dec_state->pos;
         HIP_TRY(hipHostMalloc(&c->dec_host, (size_t)c->d.max_batch_size * 4));
     }
+    // A speculative step in flight serves this call when the call continues the schedule (the
+    // position it ran at, fed the ids the previous call returned); otherwise it is undone.
+    if (c->spec_n) {
+        bool hit = L == 1 && !logits_host && c->spec_B == B && c->spec_pos[0] == start_pos && !c->timing &&
+                   (int)c->dec_last.size() == B;
+        for (int i = 0; hit && i < B; ++i) hit = c->dec_last[(size_t)i] == ids_host[i];
+        if (hit) {
+            HIP_TRY(hipEventSynchronize(c->spec_ev[0]));
+            for (int i = 0; i < B; ++i) next_ids_host[i] = c->spec_host[0][i];
+            // pop the oldest: the ring shifts by one (events and buffers travel with it)
+            hipEvent_t ev = c->spec_ev[0];
+            int32_t* hb = c->spec_host[0];
+            for (int k = 1; k < c->spec_n; ++k) {
+                c->spec_ev[k - 1] = c->spec_ev[k];
+                c->spec_host[k - 1] = c->spec_host[k];
+                c->spec_pos[k - 1] = c->spec_pos[k];
+            }
+            --c->spec_n;
+            c->spec_ev[c->spec_n] = ev;
+            c->spec_host[c->spec_n] = hb;
+            c->dec_last.assign(next_ids_host, next_ids_host + B);
+            c->dec_pos_mirror = start_pos + 1;
+            c->graph_steps++;
+            c->spec_hits++;
+            return speculate(c, B);
+        }
+        if (spec_resolve(c)) return 1;
+    }
     // Graph replay when this call continues the device-resident decode state: one token per
     // sequence at the position the state expects, fed the ids the previous step returned.
     bool replay = L == 1 && !logits_host && c->dec_exec && c->dec_B == B &&
@@ -822,7 +933,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
         c->dec_last.assign(next_ids_host, next_ids_host + B);
         c->dec_pos_mirror = start_pos + 1;
         c->graph_steps++;
-        return 0;
+        return speculate(c, B);
     }
     c->dec_pos_mirror = -1;
     if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
@@ -845,6 +956,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
         if (c->dec_B != B && capture_decode_graph(c, B)) return 1;
         c->dec_last.assign(next_ids_host, next_ids_host + B);
         c->dec_pos_mirror = next;
+        return speculate(c, B);
     }
     return 0;
 }
@@ -863,6 +975,13 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
     if (max_new_tokens > c->d.max_seq_len)
         return fail("generate: last decode position %d exceeds max_seq_len %d", max_new_tokens - 1,
                     c->d.max_seq_len);
+    if (spec_resolve(c)) return 1;
+    // the loop drives the device state itself: no speculative step between its own calls
+    struct InLoop {
+        l3_ctx* c;
+        explicit InLoop(l3_ctx* x) : c(x) { c->in_loop = true; }
+        ~InLoop() { c->in_loop = false; }
+    } in_loop(c);
     std::vector<int64_t> first((size_t)B);
     if (l3_greedy_step_host(c, ids_host, B, L, 0, first.data(), nullptr)) return 1;  // prefill
     if (steps == 1) {
@@ -938,7 +1057,7 @@ extern "C" int l3_layer_forward_host(l3_ctx* c, int32_t layer, const float* x_ho
     CHECK_CTX(c);
     if (layer < 0 || layer >= (int)c->layers.size()) return fail("layer %d out of range", layer);
     if (need_layer(c, layer, NEED_LAYER) || check_call(c, B, L, start_pos) || set_dev(c) ||
-        ensure_ws(c, B, L))
+        spec_resolve(c) || ensure_ws(c, B, L))
         return 1;
     const int64_t n = (int64_t)B * L * c->d.dim;
     HIP_TRY(hipMemcpyAsync(c->h, x_host, n * 4, hipMemcpyHostToDevice, c->stream));
@@ -955,7 +1074,7 @@ extern "C" int l3_attention_forward_host(l3_ctx* c, int32_t layer, const float* 
     CHECK_CTX(c);
     if (layer < 0 || layer >= (int)c->layers.size()) return fail("layer %d out of range", layer);
     if (need_layer(c, layer, NEED_ATTN) || check_call(c, B, L, start_pos) || set_dev(c) ||
-        ensure_ws(c, B, L))
+        spec_resolve(c) || ensure_ws(c, B, L))
         return 1;
     Layer& Ly = c->layers[layer];
     if (Ly.folded_qkv)  // this layer's wqkv carries its attention norm (full-layer context)
@@ -1191,6 +1310,13 @@ extern "C" int l3_kernel_timing(l3_ctx* c, int32_t enable) {
     for (int k = 0; k < L3_K_COUNT; ++k) { c->tot_ms[k] = 0; c->cnt[k] = 0; }
     c->timing = enable != 0;
     c->timing_mask = (unsigned)enable;
+    return 0;
+}
+
+extern "C" int l3_decode_stats(l3_ctx* c, int64_t* graph_steps, int64_t* speculative_hits) {
+    CHECK_CTX(c);
+    if (graph_steps) *graph_steps = c->graph_steps;
+    if (speculative_hits) *speculative_hits = c->spec_hits;
     return 0;
 }
 

@@ -77,6 +77,7 @@ _SIGNATURES = {
     "l3_set_batch_split": (ctypes.c_int, [_P, _I32, _I64]),
     "l3_kernel_timing": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
+    "l3_decode_stats": (ctypes.c_int, [_P, _P, _P]),
     "l3_comm_unique_id": (ctypes.c_int, [_P]),
     "l3_comm_init": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "l3_comm_gather_logits": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
@@ -300,6 +301,12 @@ class Context:
         cnt = np.zeros(len(KERNELS), np.int64)
         check(lib().l3_kernel_stats(self._h, ptr(ms), ptr(cnt)))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(KERNELS)}
+
+    def decode_stats(self) -> dict:
+        """Decode steps served by graph replay, and of those by a speculative step."""
+        v = np.zeros(2, np.int64)
+        check(lib().l3_decode_stats(self._h, ptr(v[0:1]), ptr(v[1:2])))
+        return {"graph_steps": int(v[0]), "speculative_hits": int(v[1])}
 
     # ---- RCCL ----
     def comm_init(self, nranks: int, rank: int, uid: bytes) -> None:

@@ -405,6 +405,37 @@ def test_generate_twice_and_off_schedule_steps_match_oracle(tmpdir_mod):
         ids = nxt.reshape(-1, 1)
 
 
+def test_speculative_decode_undone_when_abandoned(tmpdir_mod):
+    """The lazy generate replays each next decode step speculatively while the host yields
+    (runtime.hip: speculate / spec_resolve).  A generator abandoned mid-way leaves one step in
+    flight that appended K / V at the next position; every later call must see the cache the
+    reference's would: a new prompt whose hole (slot L, never written, llama3.py:312-318) is
+    exactly that position, then single steps off the schedule — ids exact vs the oracle making
+    the same calls."""
+    import itertools
+
+    args = synth.tiny(2)
+    w, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, 7, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(5)
+    p1 = rng.integers(0, args.vocab_size, (2, 6))
+    # 10 yields: prefill, decode at 7 (eager, arms the graph), 8..15 served speculatively; the
+    # step at 16 is in flight when the generator is dropped
+    got = np.concatenate(list(itertools.islice(m.generate(p1, 40), 10)), axis=1)
+    want = np.concatenate(list(itertools.islice(ref.generate(p1, 40), 10)), axis=1)
+    np.testing.assert_array_equal(got, want)
+    assert m.context.decode_stats()["speculative_hits"] >= 8
+    p2 = rng.integers(0, args.vocab_size, (2, 16))  # its hole is slot 16
+    got = np.concatenate(list(m.generate(p2, 30)), axis=1)
+    np.testing.assert_array_equal(got, orc.greedy_ids(ref, p2, 30))
+    ids = np.array([[3], [5]])
+    for pos in (31, 32, 30, 33):  # the step in flight ran at 30: skipped, then revisited
+        nxt, _ = m.context.greedy_step(ids, pos)
+        np.testing.assert_array_equal(nxt, ref(ids, pos)[:, -1, :].argmax(-1))
+        ids = nxt.reshape(-1, 1)
+
+
 def test_generate_all_batched_matches_oracle(tmpdir_mod):
     """the batched (B>1) device-side greedy loop — hole semantics, on-device
     argmax — gives the reference's ids for every row, on the GQA tiny model (B=3) and on

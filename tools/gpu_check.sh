@@ -48,9 +48,10 @@ for s in "$@"; do
     decgs4) L3_DECODE_GRAPH_STEPS=4 step decgs4 300 python tools/bench_decode.py ;;
     decgs16) L3_DECODE_GRAPH_STEPS=16 step decgs16 300 python tools/bench_decode.py ;;
     decgs32) L3_DECODE_GRAPH_STEPS=32 step decgs32 300 python tools/bench_decode.py ;;
+    decspec0) L3_DECODE_SPECULATE=0 step decspec0 300 python tools/bench_decode.py ;;
     declayer0) L3_DECODE_LAYER=0 step declayer0 300 python tools/bench_decode.py ;;
     decnofuse) L3_DECODE_FUSE_O=0 step decnofuse 300 python tools/bench_decode.py ;;
-    testsdec) step testsdec 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "greedy or generate or decode or head_dims or cli or cache_edges or tiny or golden" --timeout 300 --timeout-method thread ;;
+    testsdec) step testsdec 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "greedy or generate or decode or head_dims or cli or cache_edges or tiny or golden or speculative" --timeout 300 --timeout-method thread ;;
     decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
