@@ -187,6 +187,10 @@ int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
  * served by a captured-graph replay, and of those the ones a speculative step (launched when
  * the previous l3_greedy_step_host returned) answered. */
 int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits);
+/* Lazy greedy decode runs up to 16 steps ahead of the caller on the device (undone if the
+ * caller leaves the schedule, so results are unchanged); no step at position >= end_pos is run
+ * ahead (Llama.generate passes its max_new_tokens, llama3.py:312).  end_pos <= 0: no horizon. */
+int l3_set_decode_horizon(l3_ctx* ctx, int32_t end_pos);
 
 /* ---- multi-GPU: batch-sharded prefill + RCCL logits gather (xGMI) -------- */
 /* 128-byte RCCL unique id (rank 0 creates, every rank receives it). */

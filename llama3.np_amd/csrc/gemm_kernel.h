@@ -658,9 +658,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                               ? reinterpret_cast<float2*>(p.q_out + (int64_t)m * qdim + col)
                               : reinterpret_cast<float2*>((qkv_sec == 1 ? p.cache_k : p.cache_v) +
                                                           (((int64_t)bidx * p.KVH + qkv_head) * p.Smax + pos) * p.HD + qkv_d);
-            if (p.kv_bak && qkv_sec > 0)  // [pos parity][k, v][batch row][KV head][HD]
-                *reinterpret_cast<float2*>(p.kv_bak + (((((int64_t)(pos & 1) * 2 + qkv_sec - 1) * (p.M / p.L) + bidx) * p.KVH +
-                                                        qkv_head) * p.HD + qkv_d)) = bak_old[mi];
+            if (p.kv_bak && qkv_sec > 0)  // [pos % KV_BAK_SLOTS][k, v][batch row][KV head][HD]
+                *reinterpret_cast<float2*>(p.kv_bak + (((((int64_t)(pos % KV_BAK_SLOTS) * 2 + qkv_sec - 1) * (p.M / p.L) + bidx) *
+                                                        p.KVH + qkv_head) * p.HD + qkv_d)) = bak_old[mi];
             *dst = qkv_sec == 0 ? float2{r0 * p.q_scale, r1 * p.q_scale} : float2{r0, r1};
         } else {
             float* dst = p.C + (int64_t)m * p.ldc + unit;

@@ -28,9 +28,9 @@ struct GemmArgs {
     int L, start_pos, H, KVH, HD, Smax;
     const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
-    // EPI_QKV on the GEMV (captured batch-1..8 decode step): before appending K / V at pos, keep
-    // the slot's previous contents in kv_bak [pos & 1][2: k, v][M][KVH][HD], so a speculatively
-    // run decode step (two in flight: consecutive positions) can be undone (runtime.hip)
+    // EPI_QKV on the GEMV (captured batch-1..8 decode steps): before appending K / V at pos, keep
+    // the slot's previous contents in kv_bak [pos % KV_BAK_SLOTS][2: k, v][M][KVH][HD], so decode
+    // steps run ahead of the caller can be undone (runtime.hip, speculate / spec_resolve)
     float* kv_bak;
     unsigned long long* stamps;    // diagnostic builds only (STAMP template flag): 10 per block
     // Embedding fused into layer 0 (llama3.py:287): when set, A row r is A + a_rows[r] * lda
@@ -44,6 +44,7 @@ struct GemmArgs {
     const float* parts; int nparts;
 };
 constexpr int GEMV_MAXP = 8;
+constexpr int KV_BAK_SLOTS = 32;  // > the decode steps ever run ahead (runtime.hip SPEC_AHEAD)
 
 // Device-resident state of the greedy decode loop (graph replay).  pos is first, so &st->pos
 // is the pos_dev the captured kernels read.

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <deque>
 #include <vector>
 
 #include "../../include/llama3hip.h"
@@ -146,20 +147,27 @@ struct l3_ctx {
     int64_t dec_pos_mirror = -1;     // host copy of *dec_pos; -1 = device decode state invalid
     std::vector<int64_t> dec_last;   // ids the device state holds (last returned)
     int64_t graph_steps = 0;         // decode steps served by graph replay (stats)
-    // Speculative decode (lazy generate): when a step returns, the next SPEC_DEPTH steps are
-    // already queued as graph replays (the ids chain on the device), so the GPU keeps running
-    // while the host yields; each captured step keeps the K / V slot it overwrites in kv_bak
-    // (one copy per position parity), and a call that does not continue the schedule restores
-    // the slots of every step still pending
-    static constexpr int SPEC_DEPTH = 2;
-    float* kv_bak = nullptr;         // [n_layers][2 parities][2: k, v][8][KVH][HD]
+    // Run-ahead decode (lazy generate): when a step returns, up to SPEC_AHEAD further decode
+    // steps are already queued as replays of the captured step graphs (the ids chain on the
+    // device; each step's ids land in spec_hist by position), so the GPU keeps running while the
+    // host yields.  Every captured QKV append first keeps the slot it overwrites in kv_bak; a call
+    // that does not continue the schedule restores the slots of every step not yet handed out.
+    static constexpr int SPEC_AHEAD = 16;
+    float* kv_bak = nullptr;         // [n_layers][KV_BAK_SLOTS][2: k, v][8][KVH][HD]
     bool bak_capture = false;        // run_layer: QKV launches keep the overwritten slot
     bool dec_bak = false;            // the captured single-step graph keeps it
+    bool dec_n_bak = false;          // ... and the multi-step graph
     bool in_loop = false;            // generate_all drives the device state itself
-    int spec_n = 0, spec_B = 0;      // steps in flight (oldest first), their batch
-    int spec_pos[SPEC_DEPTH] = {0, 0};
-    int32_t* spec_host[SPEC_DEPTH] = {nullptr, nullptr};  // pinned: each step's ids
-    hipEvent_t spec_ev[SPEC_DEPTH] = {nullptr, nullptr};
+    int32_t* spec_hist = nullptr;    // device [max_seq_len][8]: each run-ahead step's ids
+    int32_t* spec_ids = nullptr;     // pinned mirror, copied chunk by chunk
+    bool spec_hist_armed = false;    // DecState.hist points at spec_hist
+    DecState* hist_host = nullptr;   // pinned staging of the DecState hist fields
+    int spec_base = 0, spec_end = 0; // queued steps cover positions [spec_base, spec_end)
+    int spec_B = 0;
+    int spec_limit = 0x7fffffff;     // l3_set_decode_horizon: no step at or past this position
+    struct SpecChunk { int pos0, n; hipEvent_t ev; bool done; };
+    std::deque<SpecChunk> spec_q;
+    std::vector<hipEvent_t> spec_free;  // event pool
     int64_t spec_hits = 0;
 };
 
@@ -373,10 +381,11 @@ extern "C" int l3_destroy(l3_ctx* c) {
     drop_decode_graph(c);
     dfree(c->dec_ids); dfree(c->dec_state); dfree(c->kv_bak);
     if (c->dec_host) (void)hipHostFree(c->dec_host);
-    for (int i = 0; i < l3_ctx::SPEC_DEPTH; ++i) {
-        if (c->spec_ev[i]) (void)hipEventDestroy(c->spec_ev[i]);
-        if (c->spec_host[i]) (void)hipHostFree(c->spec_host[i]);
-    }
+    for (auto& q : c->spec_q) (void)hipEventDestroy(q.ev);
+    for (hipEvent_t e : c->spec_free) (void)hipEventDestroy(e);
+    dfree(c->spec_hist);
+    if (c->spec_ids) (void)hipHostFree(c->spec_ids);
+    if (c->hist_host) (void)hipHostFree(c->hist_host);
     for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i) {
         if (c->aux[i]) { (void)hipStreamSynchronize(c->aux[i]); (void)hipStreamDestroy(c->aux[i]); }
         if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
@@ -519,7 +528,9 @@ static int need_model(l3_ctx* c) {
 extern "C" int l3_reset_cache(l3_ctx* c) {
     CHECK_CTX(c);
     if (set_dev(c)) return 1;
-    c->spec_n = 0;  // the whole cache is cleared: nothing to restore
+    for (auto& q : c->spec_q) c->spec_free.push_back(q.ev);  // the whole cache is cleared
+    c->spec_q.clear();
+    c->spec_base = c->spec_end = 0;
     c->dec_pos_mirror = -1;
     const int64_t cache = (int64_t)c->d.max_batch_size * c->d.n_kv_heads * c->d.max_seq_len * c->HD * 4;
     for (auto& L : c->layers) {
@@ -574,7 +585,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     g.pos_dev = pos_dev;
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     if (emb_ids) { g.A = c->emb; g.a_rows = emb_ids; }
-    if (c->bak_capture) g.kv_bak = c->kv_bak + (int64_t)li * 2 * 2 * 8 * c->d.n_kv_heads * c->HD;
+    if (c->bak_capture) g.kv_bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD;
     if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
     GemmArgs gu{};  // rmsnorm -> gate|up -> SwiGLU
     gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
@@ -811,62 +822,25 @@ static bool speculation_on() {
     return on;
 }
 
+// B <= 8 with run-ahead on: every QKV of a step runs on the GEMV, whose epilogue keeps the
+// overwritten slot (GemmArgs::kv_bak)
+static int bak_wanted(l3_ctx* c, int B) {
+    if (!speculation_on() || B > 8) return 0;
+    if (!c->kv_bak)
+        HIP_TRY(hipMalloc(&c->kv_bak, (size_t)c->layers.size() * KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD * 4));
+    return 1;
+}
+
 static int capture_decode_graph(l3_ctx* c, int B) {
     drop_decode_graph(c);
-    // B <= 8: every QKV of the step runs on the GEMV, whose epilogue keeps the overwritten slot
-    const bool bak = speculation_on() && B <= 8;
-    if (bak && !c->kv_bak)
-        HIP_TRY(hipMalloc(&c->kv_bak, (size_t)c->layers.size() * 2 * 2 * 8 * c->d.n_kv_heads * c->HD * 4));
+    const int bak = bak_wanted(c, B);
+    if (bak < 0) return 1;
     c->bak_capture = bak;
     const int rc = capture_steps(c, B, 1, &c->dec_graph, &c->dec_exec);
     c->bak_capture = false;
     if (rc) return 1;
     c->dec_B = B;
     c->dec_bak = bak;
-    return 0;
-}
-
-// Queue captured steps until SPEC_DEPTH are in flight, each at the position after the last
-// (dec_pos_mirror is the position the device state will reach); their ids land in spec_host
-// behind spec_ev.
-static int speculate(l3_ctx* c, int B) {
-    if (!speculation_on() || c->in_loop || !c->dec_exec || !c->dec_bak || c->dec_B != B || c->timing ||
-        c->dec_pos_mirror < 0)
-        return 0;
-    while (c->spec_n < l3_ctx::SPEC_DEPTH) {
-        const int pos = (int)c->dec_pos_mirror + c->spec_n;
-        if (pos >= c->d.max_seq_len) break;
-        const int k = c->spec_n;
-        if (!c->spec_ev[k]) HIP_TRY(hipEventCreateWithFlags(&c->spec_ev[k], hipEventDisableTiming));
-        if (!c->spec_host[k]) HIP_TRY(hipHostMalloc(&c->spec_host[k], (size_t)c->d.max_batch_size * 4));
-        HIP_TRY(hipGraphLaunch(c->dec_exec, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->spec_host[k], c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipEventRecord(c->spec_ev[k], c->stream));
-        c->spec_pos[k] = pos;
-        c->spec_B = B;
-        ++c->spec_n;
-    }
-    return 0;
-}
-
-// Undo the speculative steps nobody asked for: put back the K / V slot each appended in every
-// layer (stream-ordered after them) and drop the device decode state (the next eager step
-// re-arms it).  Every entry point that reads the cache calls this first, so the cache always
-// holds what the reference's would.
-static int spec_resolve(l3_ctx* c) {
-    if (!c->spec_n) return 0;
-    HIP_TRY(hipSetDevice(c->device));
-    const int KVH = c->d.n_kv_heads, HD = c->HD, n = c->spec_B * KVH * HD;
-    for (int k = c->spec_n - 1; k >= 0; --k) {
-        const int pos = c->spec_pos[k];
-        for (size_t li = 0; li < c->layers.size(); ++li) {
-            const float* bak = c->kv_bak + (int64_t)li * 2 * 2 * 8 * KVH * HD + (int64_t)(pos & 1) * 2 * n;
-            HIP_TRY(launch_kv_restore(c->layers[li].cache_k, bak, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
-            HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
-        }
-    }
-    c->spec_n = 0;
-    c->dec_pos_mirror = -1;
     return 0;
 }
 
@@ -879,6 +853,99 @@ static int decode_graph_steps() {
         return v < 1 ? 1 : v > 64 ? 64 : v;
     }();
     return n;
+}
+
+// the multi-step graph of decode_graph_steps() steps for batch B (device loop and run-ahead)
+static int ensure_multi_graph(l3_ctx* c, int B) {
+    const int n = decode_graph_steps();
+    if (c->dec_n == n && c->dec_n_B == B) return 0;
+    if (c->dec_exec_n) (void)hipGraphExecDestroy(c->dec_exec_n);
+    if (c->dec_graph_n) (void)hipGraphDestroy(c->dec_graph_n);
+    c->dec_exec_n = nullptr;
+    c->dec_graph_n = nullptr;
+    c->dec_n = c->dec_n_B = 0;
+    const int bak = bak_wanted(c, B);
+    c->bak_capture = bak;
+    const int rc = capture_steps(c, B, n, &c->dec_graph_n, &c->dec_exec_n);
+    c->bak_capture = false;
+    if (rc) return 1;
+    c->dec_n = n;
+    c->dec_n_B = B;
+    c->dec_n_bak = bak;
+    return 0;
+}
+
+// Queue decode steps ahead of the caller, from the position the device state will reach next,
+// until SPEC_AHEAD are in flight or the horizon (l3_set_decode_horizon, max_seq_len) is reached:
+// whole multi-step graphs where they fit, single steps otherwise; each chunk's ids are copied to
+// spec_ids behind an event.  Only from a state a step just armed (dec_pos_mirror valid).
+static int speculate(l3_ctx* c, int B) {
+    if (!speculation_on() || c->in_loop || !c->dec_exec || !c->dec_bak || c->dec_B != B || c->timing ||
+        c->dec_pos_mirror < 0)
+        return 0;
+    const int limit = c->spec_limit < c->d.max_seq_len ? c->spec_limit : c->d.max_seq_len;
+    if (c->spec_q.empty()) {
+        if (c->dec_pos_mirror >= limit) return 0;
+        c->spec_base = c->spec_end = (int)c->dec_pos_mirror;
+        c->spec_B = B;
+        if (!c->spec_hist) {  // the stream is idle here (the step that armed the state synced)
+            HIP_TRY(hipMalloc(&c->spec_hist, (size_t)c->d.max_seq_len * 8 * 4));
+            HIP_TRY(hipHostMalloc(&c->spec_ids, (size_t)c->d.max_seq_len * 8 * 4, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc(&c->hist_host, sizeof(DecState), hipHostMallocDefault));
+        }
+        if (ensure_multi_graph(c, B)) return 1;  // captured while the stream is idle
+        if (!c->spec_hist_armed) {  // argmax records every step's ids at row pos of spec_hist
+            c->hist_host->hist_base = 0;
+            c->hist_host->hist_cap = c->d.max_seq_len;
+            c->hist_host->arrive = 0;
+            c->hist_host->hist = c->spec_hist;
+            const size_t off = offsetof(DecState, hist_base);
+            HIP_TRY(hipMemcpyAsync(reinterpret_cast<char*>(c->dec_state) + off,
+                                   reinterpret_cast<char*>(c->hist_host) + off, sizeof(DecState) - off,
+                                   hipMemcpyHostToDevice, c->stream));
+            c->spec_hist_armed = true;
+        }
+    }
+    const int n = c->dec_n_bak && c->dec_n_B == B ? c->dec_n : 1;
+    while (c->spec_end - c->spec_base < l3_ctx::SPEC_AHEAD && c->spec_end < limit) {
+        const int k = n > 1 && limit - c->spec_end >= n && c->spec_end - c->spec_base + n <= l3_ctx::SPEC_AHEAD ? n : 1;
+        HIP_TRY(hipGraphLaunch(k > 1 ? c->dec_exec_n : c->dec_exec, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->spec_ids + (size_t)c->spec_end * B, c->spec_hist + (size_t)c->spec_end * B,
+                               (size_t)k * B * 4, hipMemcpyDeviceToHost, c->stream));
+        hipEvent_t ev;
+        if (c->spec_free.empty()) {
+            HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        } else {
+            ev = c->spec_free.back();
+            c->spec_free.pop_back();
+        }
+        HIP_TRY(hipEventRecord(ev, c->stream));
+        c->spec_q.push_back({c->spec_end, k, ev, false});
+        c->spec_end += k;
+    }
+    return 0;
+}
+
+// Undo the run-ahead steps nobody asked for: put back the K / V slot each appended in every
+// layer (stream-ordered after them) and drop the device decode state (the next eager step
+// re-arms it).  Every entry point that reads the cache calls this first, so the cache always
+// holds what the reference's would.
+static int spec_resolve(l3_ctx* c) {
+    if (c->spec_q.empty()) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    const int KVH = c->d.n_kv_heads, HD = c->HD, n = c->spec_B * KVH * HD;
+    for (int pos = c->spec_base; pos < c->spec_end; ++pos) {
+        for (size_t li = 0; li < c->layers.size(); ++li) {
+            const float* bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * KVH * HD + (int64_t)(pos % KV_BAK_SLOTS) * 2 * n;
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_k, bak, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
+        }
+    }
+    for (auto& q : c->spec_q) c->spec_free.push_back(q.ev);
+    c->spec_q.clear();
+    c->spec_base = c->spec_end = 0;
+    c->dec_pos_mirror = -1;
+    return 0;
 }
 
 extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
@@ -894,24 +961,21 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
     }
     // A speculative step in flight serves this call when the call continues the schedule (the
     // position it ran at, fed the ids the previous call returned); otherwise it is undone.
-    if (c->spec_n) {
-        bool hit = L == 1 && !logits_host && c->spec_B == B && c->spec_pos[0] == start_pos && !c->timing &&
+    if (!c->spec_q.empty()) {
+        bool hit = L == 1 && !logits_host && c->spec_B == B && c->spec_base == start_pos && !c->timing &&
                    (int)c->dec_last.size() == B;
         for (int i = 0; hit && i < B; ++i) hit = c->dec_last[(size_t)i] == ids_host[i];
         if (hit) {
-            HIP_TRY(hipEventSynchronize(c->spec_ev[0]));
-            for (int i = 0; i < B; ++i) next_ids_host[i] = c->spec_host[0][i];
-            // pop the oldest: the ring shifts by one (events and buffers travel with it)
-            hipEvent_t ev = c->spec_ev[0];
-            int32_t* hb = c->spec_host[0];
-            for (int k = 1; k < c->spec_n; ++k) {
-                c->spec_ev[k - 1] = c->spec_ev[k];
-                c->spec_host[k - 1] = c->spec_host[k];
-                c->spec_pos[k - 1] = c->spec_pos[k];
+            auto& q = c->spec_q.front();  // holds position spec_base
+            if (!q.done) {
+                HIP_TRY(hipEventSynchronize(q.ev));
+                q.done = true;
             }
-            --c->spec_n;
-            c->spec_ev[c->spec_n] = ev;
-            c->spec_host[c->spec_n] = hb;
+            for (int i = 0; i < B; ++i) next_ids_host[i] = c->spec_ids[(size_t)start_pos * B + i];
+            if (++c->spec_base == q.pos0 + q.n) {
+                c->spec_free.push_back(q.ev);
+                c->spec_q.pop_front();
+            }
             c->dec_last.assign(next_ids_host, next_ids_host + B);
             c->dec_pos_mirror = start_pos + 1;
             c->graph_steps++;
@@ -976,7 +1040,8 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
         return fail("generate: last decode position %d exceeds max_seq_len %d", max_new_tokens - 1,
                     c->d.max_seq_len);
     if (spec_resolve(c)) return 1;
-    // the loop drives the device state itself: no speculative step between its own calls
+    c->spec_hist_armed = false;  // the loop points DecState.hist at its own history
+    // the loop drives the device state itself: no run-ahead step between its own calls
     struct InLoop {
         l3_ctx* c;
         explicit InLoop(l3_ctx* x) : c(x) { c->in_loop = true; }
@@ -1023,16 +1088,7 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
         return done(fail("generate: decode graph not armed"));
     // the remaining steps - 2 steps: whole dec_n-step graphs, then single-step replays
     const int n = decode_graph_steps();
-    if (n > 1 && steps - 2 >= n && (c->dec_n != n || c->dec_n_B != B)) {
-        if (c->dec_exec_n) (void)hipGraphExecDestroy(c->dec_exec_n);
-        if (c->dec_graph_n) (void)hipGraphDestroy(c->dec_graph_n);
-        c->dec_exec_n = nullptr;
-        c->dec_graph_n = nullptr;
-        c->dec_n = c->dec_n_B = 0;
-        if (capture_steps(c, B, n, &c->dec_graph_n, &c->dec_exec_n)) return done(1);
-        c->dec_n = n;
-        c->dec_n_B = B;
-    }
+    if (n > 1 && steps - 2 >= n && ensure_multi_graph(c, B)) return done(1);
     for (int i = 2; i < steps;) {
         const bool multi = n > 1 && steps - i >= n;
         if (hipGraphLaunch(multi ? c->dec_exec_n : c->dec_exec, c->stream) != hipSuccess)
@@ -1310,6 +1366,12 @@ extern "C" int l3_kernel_timing(l3_ctx* c, int32_t enable) {
     for (int k = 0; k < L3_K_COUNT; ++k) { c->tot_ms[k] = 0; c->cnt[k] = 0; }
     c->timing = enable != 0;
     c->timing_mask = (unsigned)enable;
+    return 0;
+}
+
+extern "C" int l3_set_decode_horizon(l3_ctx* c, int32_t end_pos) {
+    CHECK_CTX(c);
+    c->spec_limit = end_pos > 0 ? end_pos : 0x7fffffff;
     return 0;
 }
 

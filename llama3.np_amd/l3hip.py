@@ -78,6 +78,7 @@ _SIGNATURES = {
     "l3_kernel_timing": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
     "l3_decode_stats": (ctypes.c_int, [_P, _P, _P]),
+    "l3_set_decode_horizon": (ctypes.c_int, [_P, _I32]),
     "l3_comm_unique_id": (ctypes.c_int, [_P]),
     "l3_comm_init": (ctypes.c_int, [_P, _I32, _I32, _P]),
     "l3_comm_gather_logits": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
@@ -301,6 +302,10 @@ class Context:
         cnt = np.zeros(len(KERNELS), np.int64)
         check(lib().l3_kernel_stats(self._h, ptr(ms), ptr(cnt)))
         return {k: (float(ms[i]), int(cnt[i])) for i, k in enumerate(KERNELS)}
+
+    def set_decode_horizon(self, end_pos: int) -> None:
+        """Lazy decode runs ahead of the caller on the device; never at positions >= end_pos."""
+        check(lib().l3_set_decode_horizon(self._h, int(end_pos)))
 
     def decode_stats(self) -> dict:
         """Decode steps served by graph replay, and of those by a speculative step."""

@@ -303,9 +303,12 @@ class Llama:
     def generate(self, input_ids, max_new_tokens: int) -> Iterator[np.ndarray]:
         """Greedy decode with the reference's exact position schedule
         (llama3.py:310-321): prefill at 0, then decode step i >= 1 at pos = L + i,
-        so KV slot L is never written and stays zero (the "decode hole")."""
+        so KV slot L is never written and stays zero (the "decode hole").  Lazy as the
+        reference's: the device may run up to 16 steps ahead of the consumer (never past
+        max_new_tokens), and a schedule left early is undone before any later call."""
         ids = np.asarray(input_ids)
         _, L = ids.shape
+        self._ctx.set_decode_horizon(max_new_tokens)
         next_id = None
         for i, curr_pos in enumerate(range(L, max_new_tokens)):
             if i == 0:
