@@ -44,18 +44,28 @@ static hipError_t launch_gemv_parts(const GemmArgs& a, hipStream_t s) {
     }
 }
 
-// lanes per unit from K: ~5-8 float4 per lane per W row in one chunk at the stories15M sizes
+// lanes per unit from K: ~5-8 float4 per lane per W row in one chunk at the stories15M sizes;
+// L3_GEMV_LPU=16/32/64 forces it (A/B tuning of the decode GEMVs)
+static int gemv_lpu(const GemmArgs& a) {
+    static const int force = [] { const char* e = getenv("L3_GEMV_LPU"); return e ? atoi(e) : 0; }();
+    if (force == 16 || force == 32 || force == 64) return force;
+    const int k4 = a.K / 4;
+    return k4 <= 128 ? 16 : k4 <= 256 ? 32 : 64;
+}
+
 template <int EPI, int MR>
 static hipError_t launch_gemv_mr(const GemmArgs& a, hipStream_t s) {
-    // L3_GEMV_LPU=16/32/64 forces the lanes per unit (A/B tuning of the decode GEMVs)
-    static const int force = [] { const char* e = getenv("L3_GEMV_LPU"); return e ? atoi(e) : 0; }();
-    if (force == 16) return launch_gemv_lpu<EPI, MR, 16>(a, s);
-    if (force == 32) return launch_gemv_lpu<EPI, MR, 32>(a, s);
-    if (force == 64) return launch_gemv_lpu<EPI, MR, 64>(a, s);
-    const int k4 = a.K / 4;
-    if (k4 <= 128) return launch_gemv_lpu<EPI, MR, 16>(a, s);
-    if (k4 <= 256) return launch_gemv_lpu<EPI, MR, 32>(a, s);
-    return launch_gemv_lpu<EPI, MR, 64>(a, s);
+    switch (gemv_lpu(a)) {
+        case 16: return launch_gemv_lpu<EPI, MR, 16>(a, s);
+        case 32: return launch_gemv_lpu<EPI, MR, 32>(a, s);
+        default: return launch_gemv_lpu<EPI, MR, 64>(a, s);
+    }
+}
+
+int gemv_store_blocks(const GemmArgs& a) {
+    if (a.M != 1 || !gemv_direct(a)) return 0;
+    const int per_block = 4 * (64 / gemv_lpu(a));
+    return (a.N + per_block - 1) / per_block;
 }
 
 template <int EPI>
@@ -107,6 +117,7 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
             default: return hipErrorInvalidValue;
         }
     }
+    if (a.amax_part && (epi != EPI_STORE || !gemv_store_blocks(a))) return hipErrorInvalidValue;
     if (gemm_is_gemv(a)) {
         switch (epi) {
             case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);

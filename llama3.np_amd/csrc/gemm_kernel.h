@@ -639,6 +639,31 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) acc[r][m] = group_sum<LPU>(acc[r][m]);
     }
+    if constexpr (EPI == EPI_STORE && MR == 1) {
+        if (p.amax_part) {  // batch-1 lm_head: this block's (value, index) argmax (llama3.py:320)
+            // every lane of a unit holds its sum; the value is the logit stored below, bit for bit
+            const float sc = p.norm ? __builtin_amdgcn_rsqf(ss[0] / (float)p.K + p.eps) : 1.0f;
+            float bv = valid ? acc[0][0] * sc : -INFINITY;
+            int bi = valid ? unit : 0x7fffffff;
+            group_argmax<64>(bv, bi, lane);
+            __shared__ float sv[4];
+            __shared__ int si[4];
+            if (lane == 0) {
+                sv[wid] = bv;
+                si[wid] = bi;
+            }
+            __syncthreads();
+            if (tid == 0) {
+#pragma unroll
+                for (int w2 = 1; w2 < 4; ++w2)
+                    if (argmax_better(sv[w2], si[w2], bv, bi)) {
+                        bv = sv[w2];
+                        bi = si[w2];
+                    }
+                p.amax_part[blockIdx.x] = ArgmaxPart{bv, bi};
+            }
+        }
+    }
     if (!writer) return;
 #pragma unroll
     for (int mi = 0; mi < MR; ++mi) {

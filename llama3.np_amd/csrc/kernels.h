@@ -13,6 +13,11 @@ enum Epilogue : int {
     EPI_QKV = 3,     // s_row * acc -> RoPE(q,k) -> q buffer + KV cache append
 };
 
+struct ArgmaxPart {
+    float v;
+    int i;
+};
+
 struct GemmArgs {
     const float* A; int64_t lda;   // A rows, row stride (floats)
     const float* W;                // [N, K] row-major
@@ -42,6 +47,9 @@ struct GemmArgs {
     // arrives as nparts (= n_heads, <= GEMV_MAXP) per-head partial rows [M][nparts][D] that the
     // GEMV adds to its A row (EPI_SWIGLU) or to its residual (EPI_RESID) in head order
     const float* parts; int nparts;
+    // EPI_STORE on the one-row GEMV (batch-1 lm_head): also the block's (value, index) argmax
+    // over its columns -> amax_part[blockIdx.x], reduced by launch_argmax_parts
+    ArgmaxPart* amax_part;
 };
 constexpr int GEMV_MAXP = 8;
 constexpr int KV_BAK_SLOTS = 32;  // > the decode steps ever run ahead (runtime.hip SPEC_AHEAD)
@@ -117,6 +125,44 @@ __device__ __forceinline__ float group_max(float v) {
     return v;
 }
 
+// np.argmax order (llama3.py:320): larger value first, ties to the lower index, a NaN beats any
+// number and the first NaN wins (a strict total order, so any reduction tree gives the same id)
+__device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi) {
+    const bool vn = v != v, bn = bv != bv;
+    if (vn || bn) return vn && (!bn || i < bi);
+    return v > bv || (v == bv && i < bi);
+}
+
+// (value, index) argmax over aligned groups of LANES lanes on the VALU (the group_sum pattern of
+// kernels.h: DPP quad_perm / row mirrors, then permlane swaps); argmax_better is a strict total
+// order, so the winner does not depend on the pairing
+template <int CTRL>
+__device__ __forceinline__ int dpp_mov_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int LANES>
+__device__ __forceinline__ void group_argmax(float& best, int& bi, int lane) {
+    auto step = [&](float ov, int oi) {
+        if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+    };
+    step(__int_as_float(dpp_mov_i<0xB1>(__float_as_int(best))), dpp_mov_i<0xB1>(bi));
+    step(__int_as_float(dpp_mov_i<0x4E>(__float_as_int(best))), dpp_mov_i<0x4E>(bi));
+    step(__int_as_float(dpp_mov_i<0x141>(__float_as_int(best))), dpp_mov_i<0x141>(bi));
+    step(__int_as_float(dpp_mov_i<0x140>(__float_as_int(best))), dpp_mov_i<0x140>(bi));
+    if constexpr (LANES >= 32) {  // lane i of the swapped pair: {own, lane ^ 16}, partner second in rows 0, 2
+        const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+        const auto x = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
+        const bool hi = lane & 16;
+        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
+    }
+    if constexpr (LANES >= 64) {
+        const auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+        const auto x = __builtin_amdgcn_permlane32_swap((unsigned)bi, (unsigned)bi, false, false);
+        const bool hi = lane & 32;
+        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
+    }
+}
+
 // row r of A (identity, or the gathered embedding row)
 __device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
     return p.A + (p.a_rows ? (int64_t)p.a_rows[r] : r) * p.lda;
@@ -151,6 +197,11 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
                          DecState* st = nullptr);
+// the same result from the lm_head's per-block partials (one row: GemmArgs::amax_part)
+hipError_t launch_argmax_parts(const ArgmaxPart* parts, int nparts, int32_t* out, hipStream_t s,
+                               DecState* st = nullptr);
+// blocks of the one-row lm_head GEMV (= its partial count when amax_part is set), 0 otherwise
+int gemv_store_blocks(const GemmArgs& a);
 // true when launch_gemm runs this shape on the row-blocked GEMV (short M)
 bool gemm_is_gemv(const GemmArgs& a);
 // true when that GEMV runs one row per block with the input row read per lane (the only form

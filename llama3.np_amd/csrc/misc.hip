@@ -23,72 +23,13 @@ __device__ __forceinline__ float wave_max(float v) {
 // its float4 loads in flight at once (8 per thread at the 32000-wide vocab), then a wavefront
 // butterfly and a 16-way LDS step — a decode step waits on one memory round trip, not on a
 // serial walk of the row.
-__device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi) {
-    const bool vn = v != v, bn = bv != bv;
-    if (vn || bn) return vn && (!bn || i < bi);
-    return v > bv || (v == bv && i < bi);
-}
-
-// (value, index) argmax over aligned groups of LANES lanes on the VALU (the group_sum pattern of
-// kernels.h: DPP quad_perm / row mirrors, then permlane swaps); argmax_better is a strict total
-// order, so the winner does not depend on the pairing
-template <int CTRL>
-__device__ __forceinline__ int dpp_mov_i(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
-}
-template <int LANES>
-__device__ __forceinline__ void group_argmax(float& best, int& bi, int lane) {
-    auto step = [&](float ov, int oi) {
-        if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
-    };
-    step(__int_as_float(dpp_mov_i<0xB1>(__float_as_int(best))), dpp_mov_i<0xB1>(bi));
-    step(__int_as_float(dpp_mov_i<0x4E>(__float_as_int(best))), dpp_mov_i<0x4E>(bi));
-    step(__int_as_float(dpp_mov_i<0x141>(__float_as_int(best))), dpp_mov_i<0x141>(bi));
-    step(__int_as_float(dpp_mov_i<0x140>(__float_as_int(best))), dpp_mov_i<0x140>(bi));
-    if constexpr (LANES >= 32) {  // lane i of the swapped pair: {own, lane ^ 16}, partner second in rows 0, 2
-        const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(best), __float_as_uint(best), false, false);
-        const auto x = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
-        const bool hi = lane & 16;
-        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
-    }
-    if constexpr (LANES >= 64) {
-        const auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
-        const auto x = __builtin_amdgcn_permlane32_swap((unsigned)bi, (unsigned)bi, false, false);
-        const bool hi = lane & 32;
-        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
-    }
-}
-
-__global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ x, int n,
-                                                      int32_t* __restrict__ out,
-                                                      DecState* __restrict__ st) {
-    constexpr int NT = 1024, U = 8;
-    const float* row = x + (int64_t)blockIdx.x * n;
+// block-wide finish of a row argmax (1024 threads, every thread's candidate in best / bi): the
+// id to out[blockIdx.x]; in a captured decode step also the generate history and the position
+// advance (last-arriving row)
+__device__ __forceinline__ void argmax_finish(float best, int bi, int32_t* __restrict__ out,
+                                              DecState* __restrict__ st) {
+    constexpr int NT = 1024;
     const int tid = threadIdx.x;
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-    if ((n & 3) == 0) {  // 16-byte rows
-        const int n4 = n >> 2;
-        for (int base = 0; base < n4; base += NT * U) {
-            f32x4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int f = base + u * NT + tid;
-                v[u] = f < n4 ? reinterpret_cast<const f32x4*>(row)[f] : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int f = base + u * NT + tid;
-                if (f < n4)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (argmax_better(v[u][r], 4 * f + r, best, bi)) { best = v[u][r]; bi = 4 * f + r; }
-            }
-        }
-    } else {
-        for (int i = tid; i < n; i += NT)
-            if (argmax_better(row[i], i, best, bi)) { best = row[i]; bi = i; }
-    }
     group_argmax<64>(best, bi, tid & 63);
     __shared__ float sv[NT / 64];
     __shared__ int si[NT / 64];
@@ -122,6 +63,62 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
             }
         }
     }
+}
+
+__global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ x, int n,
+                                                      int32_t* __restrict__ out,
+                                                      DecState* __restrict__ st) {
+    constexpr int NT = 1024, U = 8;
+    const float* row = x + (int64_t)blockIdx.x * n;
+    const int tid = threadIdx.x;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    if ((n & 3) == 0) {  // 16-byte rows
+        const int n4 = n >> 2;
+        for (int base = 0; base < n4; base += NT * U) {
+            f32x4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int f = base + u * NT + tid;
+                v[u] = f < n4 ? reinterpret_cast<const f32x4*>(row)[f] : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int f = base + u * NT + tid;
+                if (f < n4)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (argmax_better(v[u][r], 4 * f + r, best, bi)) { best = v[u][r]; bi = 4 * f + r; }
+            }
+        }
+    } else {
+        for (int i = tid; i < n; i += NT)
+            if (argmax_better(row[i], i, best, bi)) { best = row[i]; bi = i; }
+    }
+    argmax_finish(best, bi, out, st);
+}
+
+// one row from the batch-1 lm_head's per-block (value, index) partials (GemmArgs::amax_part):
+// 16 KB instead of the 128 KB logits row for one block to read
+__global__ void __launch_bounds__(1024) argmax_parts_kernel(const ArgmaxPart* __restrict__ parts, int n,
+                                                            int32_t* __restrict__ out,
+                                                            DecState* __restrict__ st) {
+    constexpr int NT = 1024, U = 4;
+    const int tid = threadIdx.x;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int base = 0; base < n; base += NT * U) {
+        ArgmaxPart q[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int f = base + u * NT + tid;
+            q[u] = f < n ? parts[f] : ArgmaxPart{-INFINITY, 0x7fffffff};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (argmax_better(q[u].v, q[u].i, best, bi)) { best = q[u].v; bi = q[u].i; }
+    }
+    argmax_finish(best, bi, out, st);
 }
 
 // row softmax (llama3.py:22-24): one wavefront per row, three passes over the row
@@ -192,6 +189,11 @@ static inline unsigned grid_for(int64_t n, int block) {
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
                          DecState* st) {
     hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)rows), dim3(1024), 0, s, logits, n, out, st);
+    return hipGetLastError();
+}
+hipError_t launch_argmax_parts(const ArgmaxPart* parts, int nparts, int32_t* out, hipStream_t s,
+                               DecState* st) {
+    hipLaunchKernelGGL(argmax_parts_kernel, dim3(1), dim3(1024), 0, s, parts, nparts, out, st);
     return hipGetLastError();
 }
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s) {

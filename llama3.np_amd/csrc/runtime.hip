@@ -108,6 +108,8 @@ struct l3_ctx {
     int64_t ws_T = 0, ws_B = 0;
     float *h = nullptr, *q = nullptr, *attn = nullptr, *hid = nullptr, *logits = nullptr;
     float* oparts = nullptr;         // [8, H, D] per-head O-proj rows of the fused decode attention
+    ArgmaxPart* amax_part = nullptr; // batch-1 lm_head's per-block argmax partials
+    int amax_n = 0;                  // partials the last lm_head wrote (0: none, use the logits)
     int32_t *ids = nullptr, *amax = nullptr;
     int32_t* ids_pin = nullptr;      // pinned host staging of the int32 ids (upload_ids)
     int64_t ids_pin_n = 0;
@@ -247,8 +249,9 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     drop_decode_graph(c);  // the captured graph holds workspace pointers
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits);
-    dfree(c->ids); dfree(c->amax); dfree(c->oparts);
+    dfree(c->ids); dfree(c->amax); dfree(c->oparts); dfree(c->amax_part);
     c->oparts = nullptr;
+    c->amax_part = nullptr;
     const int64_t Tn = T > c->ws_T ? T : c->ws_T;
     const int64_t Bn = B > c->ws_B ? B : c->ws_B;
     const int64_t D = c->d.dim;
@@ -261,6 +264,7 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     HIP_TRY(hipMalloc(&c->amax, Bn * 4));
     if (c->d.n_heads <= GEMV_MAXP && D <= 1024)
         HIP_TRY(hipMalloc(&c->oparts, (int64_t)8 * c->d.n_heads * D * 4));
+    HIP_TRY(hipMalloc(&c->amax_part, ((int64_t)c->d.vocab_size / 4 + 64) * sizeof(ArgmaxPart)));
     c->ws_T = Tn;
     c->ws_B = Bn;
     return 0;
@@ -373,7 +377,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     }
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
-    dfree(c->oparts);
+    dfree(c->oparts); dfree(c->amax_part);
     dfree(c->amax); dfree(c->gather_ids);
     if (c->ids_pin) (void)hipHostFree(c->ids_pin);
     for (void* p : c->scratch) dfree(p);
@@ -641,8 +645,20 @@ static GemmArgs lm_head_args(l3_ctx* c, int B, int L, float* logits_dev, int b0)
 }
 
 static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipStream_t s) {
-    const GemmArgs lm = lm_head_args(c, B, L, logits_dev, b0);
+    GemmArgs lm = lm_head_args(c, B, L, logits_dev, b0);
+    // batch 1 on the one-row GEMV: each block also leaves its (value, index) argmax, so a greedy
+    // step's argmax reads those partials instead of the whole logits row (L3_LM_AMAX=0: off)
+    static const bool amax_env = [] { const char* e = getenv("L3_LM_AMAX"); return !e || e[0] != '0'; }();
+    c->amax_n = amax_env && b0 == 0 ? gemv_store_blocks(lm) : 0;
+    if (c->amax_n) lm.amax_part = c->amax_part;
     return timed_on(c, L3_K_LMHEAD, s, [&] { return launch_gemm(EPI_STORE, lm, s); });
+}
+
+// greedy argmax of the rows the last forward left in c->logits (llama3.py:320): from the
+// lm_head's partials when it wrote them
+static hipError_t launch_greedy_argmax(l3_ctx* c, int B, DecState* st) {
+    if (c->amax_n && B == 1) return launch_argmax_parts(c->amax_part, c->amax_n, c->dec_ids, c->stream, st);
+    return launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, st);
 }
 
 
@@ -802,7 +818,7 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
     for (int i = 0; i < steps && !rc; ++i) {
         rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
         if (!rc) {
-            hipError_t e = launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, c->dec_state);
+            hipError_t e = launch_greedy_argmax(c, B, c->dec_state);
             if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
         }
     }
@@ -1002,7 +1018,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
     c->dec_pos_mirror = -1;
     if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
     if (forward_dev(c, c->ids, B, L, start_pos, c->logits)) return 1;
-    if (timed(c, L3_K_ARGMAX, [&] { return launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream); }))
+    if (timed(c, L3_K_ARGMAX, [&] { return launch_greedy_argmax(c, B, nullptr); }))
         return 1;
     HIP_TRY(hipMemcpyAsync(c->dec_host, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
     if (logits_host)
