@@ -610,6 +610,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     for (int t0 = 0; t0 < nt; t0 += CH) {
         if (t0) load_chunk(t0);
         add_parts();
+        if constexpr (XPARTS) {  // block 0's first unit holds every k4 of the summed row
+            if (p.x_out && blockIdx.x == 0 && tid < LPU) {
+#pragma unroll
+                for (int t = 0; t < CH; ++t) {
+                    const int k4 = j + LPU * (t0 + t);
+                    if (k4 < K4) reinterpret_cast<f32x4*>(p.x_out + (int64_t)m0 * p.K)[k4] = xv[t];
+                }
+            }
+        }
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             if (t0 + t >= nt) break;  // wave-uniform

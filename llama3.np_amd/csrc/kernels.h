@@ -47,6 +47,8 @@ struct GemmArgs {
     // arrives as nparts (= n_heads, <= GEMV_MAXP) per-head partial rows [M][nparts][D] that the
     // GEMV adds to its A row (EPI_SWIGLU) or to its residual (EPI_RESID) in head order
     const float* parts; int nparts;
+    float* x_out;                  // EPI_SWIGLU with parts: the summed input row (A row + parts),
+                                   // [M][K], for the down-proj's residual (written by block 0)
     // EPI_STORE on the one-row GEMV (batch-1 lm_head): also the block's (value, index) argmax
     // over its columns -> amax_part[blockIdx.x], reduced by launch_argmax_parts
     ArgmaxPart* amax_part;
@@ -169,7 +171,8 @@ __device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
 }
 // residual operand of EPI_RESID at (row, col): C itself, or the gathered embedding row
 __device__ __forceinline__ const float* res_at(const GemmArgs& p, int64_t row, int col) {
-    return p.res_src ? p.res_src + (int64_t)p.res_rows[row] * p.ldc + col : p.C + row * p.ldc + col;
+    return p.res_src ? p.res_src + (p.res_rows ? (int64_t)p.res_rows[row] : row) * p.ldc + col
+                     : p.C + row * p.ldc + col;
 }
 
 struct AttnArgs {

@@ -108,6 +108,7 @@ struct l3_ctx {
     int64_t ws_T = 0, ws_B = 0;
     float *h = nullptr, *q = nullptr, *attn = nullptr, *hid = nullptr, *logits = nullptr;
     float* oparts = nullptr;         // [8, H, D] per-head O-proj rows of the fused decode attention
+    float* hsum = nullptr;           // [8, D] h + those rows (gate|up writes it for down's residual)
     ArgmaxPart* amax_part = nullptr; // batch-1 lm_head's per-block argmax partials
     int amax_n = 0;                  // partials the last lm_head wrote (0: none, use the logits)
     int32_t *ids = nullptr, *amax = nullptr;
@@ -249,8 +250,9 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     drop_decode_graph(c);  // the captured graph holds workspace pointers
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits);
-    dfree(c->ids); dfree(c->amax); dfree(c->oparts); dfree(c->amax_part);
+    dfree(c->ids); dfree(c->amax); dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum);
     c->oparts = nullptr;
+    c->hsum = nullptr;
     c->amax_part = nullptr;
     const int64_t Tn = T > c->ws_T ? T : c->ws_T;
     const int64_t Bn = B > c->ws_B ? B : c->ws_B;
@@ -262,8 +264,10 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     HIP_TRY(hipMalloc(&c->logits, Bn * (int64_t)c->d.vocab_size * 4));
     HIP_TRY(hipMalloc(&c->ids, Tn * 4));
     HIP_TRY(hipMalloc(&c->amax, Bn * 4));
-    if (c->d.n_heads <= GEMV_MAXP && D <= 1024)
+    if (c->d.n_heads <= GEMV_MAXP && D <= 1024) {
         HIP_TRY(hipMalloc(&c->oparts, (int64_t)8 * c->d.n_heads * D * 4));
+        HIP_TRY(hipMalloc(&c->hsum, (int64_t)8 * D * 4));
+    }
     HIP_TRY(hipMalloc(&c->amax_part, ((int64_t)c->d.vocab_size / 4 + 64) * sizeof(ArgmaxPart)));
     c->ws_T = Tn;
     c->ws_B = Bn;
@@ -377,7 +381,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     }
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
-    dfree(c->oparts); dfree(c->amax_part);
+    dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum);
     dfree(c->amax); dfree(c->gather_ids);
     if (c->ids_pin) (void)hipHostFree(c->ids_pin);
     for (void* p : c->scratch) dfree(p);
@@ -604,7 +608,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     // the redundant attention of the z blocks costs more than the launch: 0.129 -> 0.134, so
     // B > 1 keeps the O-proj GEMV).  L3_DECODE_FUSE_O=0 keeps it at B = 1 too (A/B).
     static const bool fuse_env = [] { const char* e = getenv("L3_DECODE_FUSE_O"); return !e || e[0] != '0'; }();
-    const bool fuse_o = fuse_env && L == 1 && c->oparts && b0 == 0 && T == 1 && D % 4 == 0 && c->HD % 16 == 0 &&
+    const bool fuse_o = fuse_env && L == 1 && c->oparts && c->hsum && b0 == 0 && T == 1 && D % 4 == 0 && c->HD % 16 == 0 &&
                         c->d.max_seq_len <= 8192 && gemv_direct(gu) && gemv_direct(dn);
     // causal attention over the cache
     AttnArgs a{};
@@ -614,12 +618,11 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     if (fuse_o) { a.wo = Ly.wo; a.parts = c->oparts; a.D = D; }
     if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention(a, s); })) return 1;
     if (fuse_o) {
-        gu.parts = dn.parts = c->oparts;
-        gu.nparts = dn.nparts = c->d.n_heads;
-        if (emb_ids) {  // layer 0: the residual stream is still the embedding row
-            gu.A = c->emb; gu.a_rows = emb_ids;
-            dn.res_src = c->emb; dn.res_rows = emb_ids;
-        }
+        gu.parts = c->oparts;
+        gu.nparts = c->d.n_heads;
+        gu.x_out = c->hsum;  // h + attention . Wo^T, summed once by gate|up for down's residual
+        dn.res_src = c->hsum;
+        if (emb_ids) { gu.A = c->emb; gu.a_rows = emb_ids; }  // layer 0: h is the embedding row
     } else {
         // O-proj + residual (in place on h)
         GemmArgs o{};
