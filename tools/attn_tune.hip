@@ -65,6 +65,13 @@ struct Variant {
                 hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD>), grid, dim3(64 * NW), 0, s, a); \
             }}
 
+#define AV3I(NW, QBW, KT, LZ, SD)                                                             \
+    Variant{"v3ilv<w" #NW ",q" #QBW ",kt" #KT ",lazy" #LZ ",skip" #SD ">", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * NW;                                             \
+                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
+                hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD, true>), grid, dim3(64 * NW), 0, s, a); \
+            }}
+
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     srand(seed);
     for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;
@@ -153,6 +160,13 @@ int main(int argc, char** argv) {
             {AVAR(48, 4, 1, 64), AABL(32), AABL(1), AABL(2), AABL(4), AABL(8), AABL(16), AABL(18), AABL(12),
              AABL(1 | 8), AABL(1 | 4 | 8), AABL(1 | 4 | 8 | 16)},
             rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "ilv") {  // interleaved score chains
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AV3I(4, 4, 64, false, false), AV3I(4, 4, 64, false, true),
+                                  AV3I(4, 4, 64, true, true), AV3I(8, 2, 64, false, true), AV3I(8, 2, 32, false, true)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "v3") {  // lazy rescale / dead-group skip / 8 waves

@@ -14,7 +14,7 @@
 
 namespace l3 {
 
-template <int HD, int NW, int QBW, int KT, bool LAZY, bool SKIPD>
+template <int HD, int NW, int QBW, int KT, bool LAZY, bool SKIPD, bool ILV = false>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (NW == 4 || NW == 8), "shape");
     constexpr int NT = 64 * NW;
@@ -104,6 +104,27 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnA
             const int q_abs = start_pos + qblock_first + fq;
             f32x4 sacc[KG];
             bool live[KG];
+            if constexpr (ILV && !MASKED) {
+                // all key groups live: the KG accumulation chains interleaved (one MFMA of each
+                // chain in turn), the d-group's KG fragments read together
+#pragma unroll
+                for (int kg = 0; kg < KG; ++kg) {
+                    live[kg] = true;
+                    sacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int dg = 0; dg < ND; ++dg) {
+                    f32x4 kf[KG];
+#pragma unroll
+                    for (int kg = 0; kg < KG; ++kg)
+                        kf[kg] = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
+#pragma unroll
+                    for (int s = 0; s < 4; ++s)
+#pragma unroll
+                        for (int kg = 0; kg < KG; ++kg)
+                            sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[kg][s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
+                }
+            } else {
 #pragma unroll
             for (int kg = 0; kg < KG; ++kg) {
                 live[kg] = !MASKED || (k0 + kg * 16) <= qmax_abs;
@@ -117,6 +138,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnA
                             sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
                     }
                 }
+            }
             }
             float mt = -INFINITY;
 #pragma unroll
