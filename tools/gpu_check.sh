@@ -57,6 +57,7 @@ for s in "$@"; do
     decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
+    c4) step c4 300 python bench.py --global-batch 2048 --steps 5 --warmup 1 --no-cpu-baseline --no-kernel-breakdown ;;
     c5small) step c5small 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     c5small1) L3_BATCH_SPLIT=1 step c5small1 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
