@@ -14,6 +14,7 @@
 #include "attn_ring.h"
 #include "attn_variants.h"
 #include "attn_v3.h"
+#include "attn_resident.h"
 
 using namespace l3;
 
@@ -70,6 +71,13 @@ struct Variant {
                 constexpr int QW = 16 * QBW * NW;                                             \
                 dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
                 hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD, true>), grid, dim3(64 * NW), 0, s, a); \
+            }}
+
+#define AVRES(HD, KMAX, TO)                                                                   \
+    Variant{"resident<" #HD ",kmax" #KMAX ",tileouter" #TO ">", [](const AttnArgs& a, hipStream_t s) { \
+                const int items = a.B * a.H;                                                  \
+                dim3 grid(items < 256 ? items : 256);                                         \
+                hipLaunchKernelGGL((attn_resident_kernel<HD, KMAX, TO>), grid, dim3(512), 0, s, a); \
             }}
 
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
@@ -160,6 +168,14 @@ int main(int argc, char** argv) {
             {AVAR(48, 4, 1, 64), AABL(32), AABL(1), AABL(2), AABL(4), AABL(8), AABL(16), AABL(18), AABL(12),
              AABL(1 | 8), AABL(1 | 4 | 8), AABL(1 | 4 | 8 | 16)},
             rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "res") {  // K/V resident, persistent, barrier-free
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AVRES(48, 256, false), AVRES(48, 256, true)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48, v, 1, 1, 19);
+        run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "ilv") {  // interleaved score chains
