@@ -436,6 +436,45 @@ def test_speculative_decode_undone_when_abandoned(tmpdir_mod):
         ids = nxt.reshape(-1, 1)
 
 
+def test_decode_run_ahead_random_call_sequences(tmpdir_mod):
+    """Random interleavings of the calls that touch the KV cache — lazy generators dropped after
+    a random number of yields (steps queued ahead are still in flight), complete generators,
+    prefills through Llama.__call__, single greedy steps on and off the schedule, the device
+    loop — every result equal to the oracle making the same calls (the cache must always hold
+    what the reference's would, whatever the device ran ahead)."""
+    import itertools
+
+    args = synth.tiny(2)
+    w, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, 23, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(99)
+    VS, Smax = args.vocab_size, args.max_seq_len
+    for _ in range(14):
+        op = int(rng.integers(0, 5))
+        B = int(rng.integers(1, 3))
+        L = int(rng.integers(1, 24))
+        prompt = rng.integers(0, VS, (B, L))
+        if op in (0, 1):  # generator, dropped after k yields (op 0) or run to the end (op 1)
+            n = int(rng.integers(L + 2, min(Smax, L + 40)))
+            k = int(rng.integers(1, n - L)) if op == 0 else n - L
+            got = np.concatenate(list(itertools.islice(m.generate(prompt, n), k)), axis=1)
+            want = np.concatenate(list(itertools.islice(ref.generate(prompt, n), k)), axis=1)
+            np.testing.assert_array_equal(got, want)
+        elif op == 2:  # prefill at a random start position (chunked prompt)
+            sp = int(rng.integers(0, Smax - L))
+            np.testing.assert_allclose(m(prompt, sp), ref(prompt, sp), atol=1e-4, rtol=2e-4)
+        elif op == 3:  # single steps at random positions
+            ids = prompt[:, :1]
+            for pos in rng.integers(0, Smax, 3):
+                nxt, _ = m.context.greedy_step(ids, int(pos))
+                np.testing.assert_array_equal(nxt, ref(ids, int(pos))[:, -1, :].argmax(-1))
+                ids = nxt.reshape(-1, 1)
+        else:  # the device loop
+            n = int(rng.integers(L + 1, min(Smax, L + 30)))
+            np.testing.assert_array_equal(m.generate_all(prompt, n), orc.greedy_ids(ref, prompt, n))
+
+
 def test_generate_all_batched_matches_oracle(tmpdir_mod):
     """the batched (B>1) device-side greedy loop — hole semantics, on-device
     argmax — gives the reference's ids for every row, on the GQA tiny model (B=3) and on

@@ -54,7 +54,7 @@ for s in "$@"; do
     decamax0) L3_LM_AMAX=0 step decamax0 300 python tools/bench_decode.py ;;
     declayer0) L3_DECODE_LAYER=0 step declayer0 300 python tools/bench_decode.py ;;
     decnofuse) L3_DECODE_FUSE_O=0 step decnofuse 300 python tools/bench_decode.py ;;
-    testsdec) step testsdec 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "greedy or generate or decode or head_dims or cli or cache_edges or tiny or golden or speculative" --timeout 300 --timeout-method thread ;;
+    testsdec) step testsdec 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "greedy or generate or decode or head_dims or cli or cache_edges or tiny or golden or speculative or run_ahead" --timeout 300 --timeout-method thread ;;
     decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
