@@ -843,17 +843,17 @@ static bool speculation_on() {
 
 // B <= 8 with run-ahead on: every QKV of a step runs on the GEMV, whose epilogue keeps the
 // overwritten slot (GemmArgs::kv_bak)
-static int bak_wanted(l3_ctx* c, int B) {
-    if (!speculation_on() || B > 8) return 0;
-    if (!c->kv_bak)
+static int bak_wanted(l3_ctx* c, int B, bool* bak) {
+    *bak = speculation_on() && B <= 8;
+    if (*bak && !c->kv_bak)
         HIP_TRY(hipMalloc(&c->kv_bak, (size_t)c->layers.size() * KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD * 4));
-    return 1;
+    return 0;
 }
 
 static int capture_decode_graph(l3_ctx* c, int B) {
     drop_decode_graph(c);
-    const int bak = bak_wanted(c, B);
-    if (bak < 0) return 1;
+    bool bak = false;
+    if (bak_wanted(c, B, &bak)) return 1;
     c->bak_capture = bak;
     const int rc = capture_steps(c, B, 1, &c->dec_graph, &c->dec_exec);
     c->bak_capture = false;
@@ -883,7 +883,8 @@ static int ensure_multi_graph(l3_ctx* c, int B) {
     c->dec_exec_n = nullptr;
     c->dec_graph_n = nullptr;
     c->dec_n = c->dec_n_B = 0;
-    const int bak = bak_wanted(c, B);
+    bool bak = false;
+    if (bak_wanted(c, B, &bak)) return 1;
     c->bak_capture = bak;
     const int rc = capture_steps(c, B, n, &c->dec_graph_n, &c->dec_exec_n);
     c->bak_capture = false;

@@ -136,6 +136,26 @@ int main(void) {
             fprintf(stderr, "FAIL generated id %lld out of range\n", (long long)out[i]);
             return 1;
         }
+    // the same schedule one step per call (the reference's lazy generator: prefill, then decode
+    // at pos 5 + i, i >= 1) with the device running ahead: the device loop's ids, step for step
+    CHECK(l3_set_decode_horizon(c, 25));
+    int64_t lz[B];
+    CHECK(l3_greedy_step_host(c, ids, B, 5, 0, lz, NULL));
+    for (int i = 0; i < 20; ++i) {
+        if (i) CHECK(l3_greedy_step_host(c, lz, B, 1, 5 + i, lz, NULL));
+        for (int b = 0; b < B; ++b)
+            if (lz[b] != out[b * 20 + i]) {
+                fprintf(stderr, "FAIL lazy step %d row %d: %lld != device loop %lld\n", i, b,
+                        (long long)lz[b], (long long)out[b * 20 + i]);
+                return 1;
+            }
+    }
+    int64_t replayed = 0, ahead = 0;
+    CHECK(l3_decode_stats(c, &replayed, &ahead));
+    if (ahead < 10) {
+        fprintf(stderr, "FAIL only %lld of the lazy steps were run ahead\n", (long long)ahead);
+        return 1;
+    }
 
     // the reference's failure modes become error returns with a message
     EXPECT_FAIL(l3_forward_host(c, ids, MB + 1, 1, 0, logits));  // batch > max_batch_size
