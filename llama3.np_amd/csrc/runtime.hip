@@ -927,8 +927,12 @@ static int speculate(l3_ctx* c, int B) {
         }
     }
     const int n = c->dec_n_bak && c->dec_n_B == B ? c->dec_n : 1;
-    while (c->spec_end - c->spec_base < l3_ctx::SPEC_AHEAD && c->spec_end < limit) {
-        const int k = n > 1 && limit - c->spec_end >= n && c->spec_end - c->spec_base + n <= l3_ctx::SPEC_AHEAD ? n : 1;
+    while (c->spec_end < limit) {
+        // whole n-step graphs (the queue refills by n once n steps have been handed out, so it
+        // holds SPEC_AHEAD - n .. SPEC_AHEAD steps); single steps only for the tail before the
+        // horizon
+        const int k = n > 1 && limit - c->spec_end >= n ? n : 1;
+        if (c->spec_end - c->spec_base + k > l3_ctx::SPEC_AHEAD) break;
         HIP_TRY(hipGraphLaunch(k > 1 ? c->dec_exec_n : c->dec_exec, c->stream));
         HIP_TRY(hipMemcpyAsync(c->spec_ids + (size_t)c->spec_end * B, c->spec_hist + (size_t)c->spec_end * B,
                                (size_t)k * B * 4, hipMemcpyDeviceToHost, c->stream));
