@@ -844,7 +844,11 @@ static bool speculation_on() {
 // B <= 8 with run-ahead on: every QKV of a step runs on the GEMV, whose epilogue keeps the
 // overwritten slot (GemmArgs::kv_bak)
 static int bak_wanted(l3_ctx* c, int B, bool* bak) {
-    *bak = speculation_on() && B <= 8;
+    GemmArgs qkv{};  // the shape of a decode step's QKV launch: only the GEMV keeps the slot
+    qkv.M = B;
+    qkv.N = c->qkvn;
+    qkv.K = c->d.dim;
+    *bak = speculation_on() && B <= 8 && gemm_is_gemv(qkv);
     if (*bak && !c->kv_bak)
         HIP_TRY(hipMalloc(&c->kv_bak, (size_t)c->layers.size() * KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD * 4));
     return 0;

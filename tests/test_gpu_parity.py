@@ -475,6 +475,31 @@ def test_decode_run_ahead_random_call_sequences(tmpdir_mod):
             np.testing.assert_array_equal(m.generate_all(prompt, n), orc.greedy_ids(ref, prompt, n))
 
 
+def test_run_ahead_needs_the_gemv_qkv(tmpdir_mod):
+    """Run-ahead undoes its steps from the slots the QKV GEMV's epilogue saved; where a decode
+    step's QKV runs on the MFMA tiles instead (here D = 2304 at B = 8: 8 rows x K past the GEMV's
+    row block) there is no saved slot, so nothing may run ahead — a dropped generator followed by
+    a prompt whose hole is the next position still matches the oracle, with no speculative hit."""
+    import itertools
+
+    from config import ModelArgs
+
+    args = ModelArgs(dim=2304, n_layers=1, n_heads=18, n_kv_heads=6, vocab_size=512, max_seq_len=48,
+                     max_batch_size=8)
+    w, path = _model(tmpdir_mod, args, 256, 31, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(3)
+    p1 = rng.integers(0, args.vocab_size, (8, 5))
+    got = np.concatenate(list(itertools.islice(m.generate(p1, 30), 8)), axis=1)
+    want = np.concatenate(list(itertools.islice(ref.generate(p1, 30), 8)), axis=1)
+    np.testing.assert_array_equal(got, want)
+    assert m.context.decode_stats()["speculative_hits"] == 0
+    p2 = rng.integers(0, args.vocab_size, (8, 13))  # its hole is slot 13, one past the last step
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(p2, 20)), axis=1),
+                                  orc.greedy_ids(ref, p2, 20))
+
+
 def test_generate_all_batched_matches_oracle(tmpdir_mod):
     """the batched (B>1) device-side greedy loop — hole semantics, on-device
     argmax — gives the reference's ids for every row, on the GQA tiny model (B=3) and on
