@@ -73,6 +73,13 @@ struct Variant {
                 hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD, true>), grid, dim3(64 * NW), 0, s, a); \
             }}
 
+#define AV3P(NW, QBW, KT, LZ, SD)                                                             \
+    Variant{"v3pipe<w" #NW ",q" #QBW ",kt" #KT ",lazy" #LZ ",skip" #SD ">", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * NW;                                             \
+                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
+                hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD, true, true>), grid, dim3(64 * NW), 0, s, a); \
+            }}
+
 #define AVRES(HD, KMAX, TO)                                                                   \
     Variant{"resident<" #HD ",kmax" #KMAX ",tileouter" #TO ">", [](const AttnArgs& a, hipStream_t s) { \
                 const int items = a.B * a.H;                                                  \
@@ -168,6 +175,13 @@ int main(int argc, char** argv) {
             {AVAR(48, 4, 1, 64), AABL(32), AABL(1), AABL(2), AABL(4), AABL(8), AABL(16), AABL(18), AABL(12),
              AABL(1 | 8), AABL(1 | 4 | 8), AABL(1 | 4 | 8 | 16)},
             rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "pipe") {  // LDS reads one group ahead
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AV3I(4, 4, 64, false, true), AV3P(4, 4, 64, false, true),
+                                  AV3P(4, 4, 64, true, true)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "res") {  // K/V resident, persistent, barrier-free

@@ -14,7 +14,7 @@
 
 namespace l3 {
 
-template <int HD, int NW, int QBW, int KT, bool LAZY, bool SKIPD, bool ILV = false>
+template <int HD, int NW, int QBW, int KT, bool LAZY, bool SKIPD, bool ILV = false, bool PIPE = false>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (NW == 4 || NW == 8), "shape");
     constexpr int NT = 64 * NW;
@@ -112,6 +112,33 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnA
                     live[kg] = true;
                     sacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
                 }
+                if constexpr (PIPE) {
+                    // fragments of d-group dg + 1 read while d-group dg's 16 MFMAs issue; the
+                    // order pinned by scheduling groups (DS read x KG, then MFMA x 16)
+                    f32x4 kf[2][KG];
+#pragma unroll
+                    for (int kg = 0; kg < KG; ++kg)
+                        kf[0][kg] = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][fk]);
+#pragma unroll
+                    for (int dg = 0; dg < ND; ++dg) {
+                        if (dg + 1 < ND) {
+#pragma unroll
+                            for (int kg = 0; kg < KG; ++kg)
+                                kf[(dg + 1) & 1][kg] = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][(dg + 1) * 16 + fk]);
+                        }
+#pragma unroll
+                        for (int s = 0; s < 4; ++s)
+#pragma unroll
+                            for (int kg = 0; kg < KG; ++kg)
+                                sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[dg & 1][kg][s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x100, KG, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, KG, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4 * KG, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, KG, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4 * KG, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 4 * KG, 0);
+                } else {
 #pragma unroll
                 for (int dg = 0; dg < ND; ++dg) {
                     f32x4 kf[KG];
@@ -123,6 +150,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnA
 #pragma unroll
                         for (int kg = 0; kg < KG; ++kg)
                             sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[kg][s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
+                }
                 }
             } else {
 #pragma unroll
@@ -191,6 +219,29 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnA
                 }
             }
             l_run[j] += psum;
+            if constexpr (PIPE && !MASKED) {
+                // V values of key group kg + 1 read while kg's 12 MFMAs issue
+                float vv[2][ND][4];
+#pragma unroll
+                for (int dg = 0; dg < ND; ++dg)
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2) vv[0][dg][s2] = Vs[cur][fk + s2][dg * 16 + fq];
+#pragma unroll
+                for (int kg = 0; kg < KG; ++kg) {
+                    if (kg + 1 < KG) {
+#pragma unroll
+                        for (int dg = 0; dg < ND; ++dg)
+#pragma unroll
+                            for (int s2 = 0; s2 < 4; ++s2)
+                                vv[(kg + 1) & 1][dg][s2] = Vs[cur][(kg + 1) * 16 + fk + s2][dg * 16 + fq];
+                    }
+#pragma unroll
+                    for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+                        for (int dg = 0; dg < ND; ++dg)
+                            o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[kg & 1][dg][s2], sacc[kg][s2], o[j][dg], 0, 0, 0);
+                }
+            } else {
 #pragma unroll
             for (int kg = 0; kg < KG; ++kg) {
                 if (!live[kg]) continue;
@@ -201,6 +252,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) attn_v3_kernel(AttnA
                         const float vf = Vs[cur][kg * 16 + fk + s][dg * 16 + fq];
                         o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);
                     }
+            }
             }
         };
 #pragma unroll
