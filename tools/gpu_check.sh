@@ -78,6 +78,8 @@ for s in "$@"; do
     benchq8) GPU_MAX_HW_QUEUES=8 step benchq8 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     pmcattn) step pmcattnA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcattnA -o run --output-format csv -- tools/attn_tune 1 2 c3
            step pmcattnB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcattnB -o run --output-format csv -- tools/attn_tune 1 2 c3 ;;
+    pmcgemm) step pmcgemmA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcgemmA -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1
+             step pmcgemmB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcgemmB -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 ;;
     attnprof) step attnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attnprof -o run --output-format csv -- tools/attn_tune 3 10 ;;
     cabi) step cabi 300 python -u -m pytest tests/test_c_abi_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
