@@ -144,6 +144,96 @@ def traffic_per_launch(rows):
     return d.get("hbm_bytes_per_launch")
 
 
+def c5_context(n_layers, B, L):
+    """A Llama-3-8B-shaped context (D 4096, H 32 / KVH 8, FD 14336, VS 128256) with synthetic
+    weights uploaded tensor by tensor through the C ABI (uniform, std 0.02, drawn from a
+    256M-float pool: an 8.5G-sample normal draw would take minutes)."""
+    args = synth.llama3_shape(n_layers=n_layers, max_batch_size=B, max_seq_len=L)
+    D, FD, VS, H, KVH = args.dim, synth.LLAMA3_HIDDEN, args.vocab_size, args.n_heads, args.kv_heads
+    HD = D // H
+    dims = l3hip.Dims(dim=D, n_layers=args.n_layers, n_heads=H, n_kv_heads=KVH, vocab_size=VS,
+                      hidden_dim=FD, max_seq_len=L, max_batch_size=B, norm_eps=args.norm_eps)
+    ctx = l3hip.Context(dims, 0)
+    rng = np.random.default_rng(0)
+    pool = (rng.random(1 << 28, dtype=np.float32) * 2 - 1) * np.float32(0.02 * 3 ** 0.5)
+
+    def tensor(shape):
+        n = int(np.prod(shape))
+        if n <= pool.size:
+            o = int(rng.integers(0, pool.size - n + 1))
+            return pool[o:o + n].reshape(shape)
+        return np.resize(pool, n).reshape(shape)
+
+    ctx.upload(0, l3hip.W_EMBED, np.resize(pool * np.float32(50.0), VS * D).reshape(VS, D))
+    for i in range(args.n_layers):
+        for kind, shape in ((l3hip.W_Q, (H * HD, D)), (l3hip.W_K, (KVH * HD, D)), (l3hip.W_V, (KVH * HD, D)),
+                            (l3hip.W_O, (D, H * HD)), (l3hip.W_GATE, (FD, D)), (l3hip.W_UP, (FD, D)),
+                            (l3hip.W_DOWN, (D, FD))):
+            ctx.upload(i, kind, tensor(shape))
+        ctx.upload(i, l3hip.W_ATTN_NORM, np.ones(D, np.float32))
+        ctx.upload(i, l3hip.W_FFN_NORM, np.ones(D, np.float32))
+    ctx.upload(0, l3hip.W_FINAL_NORM, np.ones(D, np.float32))
+    ctx.upload(0, l3hip.W_LM_HEAD, tensor((VS, D)))
+    ctx.finalize()
+    return ctx, args, rng
+
+
+def bench_c5_decode(a):
+    """Greedy decode at the Llama-3-8B shape (32 layers, B = 1): a 64-token prefill, then the
+    device loop (generate_all) for a.steps + 2 tokens and the lazy one-step-per-call schedule
+    for the same tokens (ids must agree).  Decode streams every weight once per token, so the
+    roofline is HBM: weight bytes per token / time per token against 8 TB/s."""
+    B, L0 = 1, 64
+    ctx, args, rng = c5_context(a.layers, B, 2048)
+    D, FD, VS, H, KVH = args.dim, synth.LLAMA3_HIDDEN, args.vocab_size, args.n_heads, args.kv_heads
+    HD = D // H
+    ids = rng.integers(0, VS, (B, L0))
+    n = L0 + max(3, a.steps + 2)
+    # L3_DECODE_GRAPH=0 (per-kernel profiling: kernel tracing does not survive capture) has no
+    # device loop; only the lazy schedule runs then, eager step by step
+    graphs = os.environ.get("L3_DECODE_GRAPH", "1") != "0"
+    dev_ids, t_dev, t_head = None, None, None
+    if graphs:
+        ctx.greedy_generate(ids, L0 + 4)  # warm-up: captures the decode graphs
+        # decode steps only: the prefill (64 rows through the MFMA GEMMs) and the eager first
+        # step are timed on their own and taken out
+        t0 = time.perf_counter()
+        ctx.greedy_generate(ids, L0 + 2)
+        t_head = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        dev_ids = ctx.greedy_generate(ids, n)
+        t_dev = time.perf_counter() - t0 - t_head
+    ctx.set_decode_horizon(n)
+    lazy = []
+    nxt, _ = ctx.greedy_step(ids, 0)
+    lazy.append(int(nxt[0]))
+    nxt, _ = ctx.greedy_step(nxt.reshape(1, 1), L0 + 1)
+    lazy.append(int(nxt[0]))
+    t0 = time.perf_counter()
+    for i in range(2, n - L0):
+        nxt, _ = ctx.greedy_step(nxt.reshape(1, 1), L0 + i)
+        lazy.append(int(nxt[0]))
+    t_lazy = time.perf_counter() - t0
+    steps = n - L0 - 2
+    w_bytes = 4 * (args.n_layers * (D * (H + 2 * KVH) * HD + D * H * HD + 3 * D * FD) + VS * D)
+    ms = (t_dev if graphs else t_lazy) / steps * 1e3
+    print(json.dumps({
+        "metric": "ms/token Llama-3-shape greedy decode B=1 (decode path at a bandwidth-bound size)",
+        "value": round(ms, 3), "unit": "ms/token", "higher_is_better": False, "n_gpus": 1,
+        "config": {"workload": f"Llama-3-8B shape, {args.n_layers} layers, B=1, prefill {L0}, "
+                               f"{steps} timed decode steps (prefill and step 1 excluded)", "seq_len": n},
+        "device_loop_ms_per_token": round(ms, 3) if graphs else None,
+        "lazy_generate_ms_per_token": round(t_lazy / steps * 1e3, 3),
+        "ids_equal_lazy_vs_device_loop": bool(dev_ids[0].tolist() == lazy) if graphs else None,
+        "decode_graphs": graphs,
+        "prefill_and_step1_ms": round(t_head * 1e3, 3) if graphs else None,
+        "roofline": {"bound": "hbm", "achieved": round(w_bytes / (ms * 1e-3) / 1e9, 1),
+                     "peak": 8000.0, "unit": "GB/s",
+                     "frac": round(w_bytes / (ms * 1e-3) / 1e9 / 8000.0, 4),
+                     "traffic": None, "bytes_per_token": w_bytes},
+        "lib": {"version": l3hip.version(), "source_hash": l3hip.source_hash()}}))
+
+
 def bench_c5(a):
     """BASELINE configs[4]: Llama-3-8B-shaped prefill (D 4096, 32 layers, H 32 / KVH 8,
     FD 14336, VS 128256), B=64, L=2048 on one GPU — a roofline report, not the headline line.
@@ -306,9 +396,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-breakdown", action="store_true",
                     help="skip the untimed all-kernel event pass (profiling runs)")
-    ap.add_argument("--workload", choices=["c3", "c5", "c5cpu"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c5", "c5cpu", "c5decode"], default="c3",
                     help="c3: headline stories15M B=256 L=256 (default); c5: Llama-3-shape report; "
-                         "c5cpu: the oracle on a 2-layer C5 slice, extrapolated")
+                         "c5cpu: the oracle on a 2-layer C5 slice, extrapolated; c5decode: "
+                         "Llama-3-shape batch-1 greedy decode (HBM roofline)")
     ap.add_argument("--layers", type=int, default=32, help="c5 only")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="strong scaling: this many rows split over the GPUs (default: 256 per GPU)")
@@ -324,6 +415,8 @@ def main():
         return bench_c5(a)
     if a.workload == "c5cpu":
         return cpu_c5_slice()
+    if a.workload == "c5decode":
+        return bench_c5_decode(a)
 
     dist = Dist(a.gpus, force_comm=a.rccl)
     # default: weak scaling, B = 256 rows per GPU (N = 8 is C4's B = 2048); --global-batch G:

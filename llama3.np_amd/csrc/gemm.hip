@@ -18,6 +18,56 @@ static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Split-K for short M against a long K (batched decode and short prompts at Llama-3 sizes):
+// a 64-row x 4096-deep O-proj is 32 tiles of 128 columns, so 32 blocks would each stream a
+// 2 MB weight panel (C5 64-token prefill: 0.59 ms per O-proj / down launch).  The k-slices run
+// as tiles x S blocks (S a power of two up to 16, >= 8 k-tiles per slice, about 1024 blocks in
+// all) and splitk_finish_kernel sums them in slice order and applies the epilogue.
+template <int WM, int WN, int TM, int TN, int BK, int NS>
+static hipError_t launch_split_cfg(int epi, GemmArgs a, hipStream_t s) {
+    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+    const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    const int nk = a.K / BK;
+    const int64_t need_per = (int64_t)a.M * a.N + a.M;  // floats per slice
+    static const int target = [] { const char* e = getenv("L3_SPLITK_BLOCKS"); return e ? atoi(e) : 1024; }();
+    static const int min_kt = [] { const char* e = getenv("L3_SPLITK_MINKT"); return e ? atoi(e) : 8; }();
+    int S = 1;
+    while (S < 16 && tiles * S < target && nk % (2 * S) == 0 && nk / (2 * S) >= min_kt &&
+           2 * S * need_per <= a.ws_cap)
+        S *= 2;
+    if (S == 1) return hipErrorNotReady;  // not worth it: the caller runs the unsplit tiles
+    a.splits = S;
+    hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI_STORE, 2, false, BK, true, NS, true>),
+                       dim3((unsigned)(tiles * S)), dim3(256), 0, s, a);
+    if (const hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    const int64_t outs = (int64_t)a.M * (epi == EPI_SWIGLU ? a.N / 2 : a.N) / 4;
+    const dim3 grid((unsigned)((outs + 255) / 256));
+    switch (epi) {
+        case EPI_SWIGLU: hipLaunchKernelGGL(splitk_finish_kernel<EPI_SWIGLU>, grid, dim3(256), 0, s, a); break;
+        case EPI_QKV: hipLaunchKernelGGL(splitk_finish_kernel<EPI_QKV>, grid, dim3(256), 0, s, a); break;
+        case EPI_RESID: hipLaunchKernelGGL(splitk_finish_kernel<EPI_RESID>, grid, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL(splitk_finish_kernel<EPI_STORE>, grid, dim3(256), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+// L3_SPLITK=0: off (A/B); L3_SPLITK_CFG picks the slice tile (tuning)
+static hipError_t launch_split(int epi, const GemmArgs& a, hipStream_t s) {
+    static const int on = [] { const char* e = getenv("L3_SPLITK"); return e ? atoi(e) : 1; }();
+    static const int cfg = [] { const char* e = getenv("L3_SPLITK_CFG"); return e ? atoi(e) : 0; }();
+    if (!on || !a.ws || a.M <= 8 || a.M > 256 || a.K < 2048 || a.K % 32 != 0) return hipErrorNotReady;
+    switch (cfg) {
+        case 1: return launch_split_cfg<2, 2, 4, 4, 16, 2>(epi, a, s);
+        case 2: return launch_split_cfg<2, 2, 2, 4, 32, 2>(epi, a, s);
+        case 3: return launch_split_cfg<2, 2, 2, 4, 16, 4>(epi, a, s);
+        case 4: return launch_split_cfg<1, 4, 1, 2, 32, 2>(epi, a, s);
+        default:
+            if (a.M <= 16) return launch_split_cfg<1, 4, 1, 2, 32, 2>(epi, a, s);  // 16 x 128
+            if (a.M <= 64) return launch_split_cfg<2, 2, 2, 4, 32, 2>(epi, a, s);  // 64 x 128
+            return launch_split_cfg<2, 2, 4, 4, 32, 2>(epi, a, s);                 // 128 x 128
+    }
+}
+
 template <int EPI, int MR, int LPU, bool PARTS = false>
 static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
     const int units = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? a.N / 2 : a.N;
@@ -126,6 +176,10 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
             case EPI_STORE: return launch_gemv<EPI_STORE>(a, s);
             default: return hipErrorInvalidValue;
         }
+    }
+    if (a.ws) {
+        const hipError_t e = launch_split(epi, a, s);
+        if (e != hipErrorNotReady) return e;
     }
     // Configurations chosen with tools/gemm_tune (interleaved A/B on MI355X).
     // 128 x 128 BK16: 120 VGPRs + 32 KB LDS -> 4 blocks per CU.

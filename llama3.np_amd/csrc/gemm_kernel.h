@@ -177,6 +177,88 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
     }
 }
 
+// Split-K epilogue: the raw accumulators of k-slice ks to p.ws[ks][M][N] (same register-direct
+// fragment map, 16-byte stores) and, with the norm, the rows' partial sums of squares to
+// p.ws[splits * M * N + ks * M + row] (one wave column writes them)
+template <int TM, int TN>
+__device__ __forceinline__ void split_epilogue(const GemmArgs& p, const f32x4 (&acc)[TM][TN],
+                                               const float (&ss)[TM], int ks, int mrow0, int ncol0,
+                                               int lane, bool ss_writer) {
+    const int frow = lane & 15, fq4 = 4 * (lane >> 4);
+    const int64_t MN = (int64_t)p.M * p.N;
+    float* part = p.ws + ks * MN;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int row = mrow0 + i * 16 + frow;
+        const float v = sum_xor16_32(ss[i]);  // every lane takes part in the exchange
+        if (row >= p.M) continue;
+        if (p.norm && ss_writer && lane < 16) p.ws[p.splits * MN + (int64_t)ks * p.M + row] = v;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = ncol0 + j * 16 + fq4;
+            if (col < p.N) *reinterpret_cast<f32x4*>(part + (int64_t)row * p.N + col) = acc[i][j];
+        }
+    }
+}
+
+// Split-K finish: one thread per output float4 (EPI_SWIGLU: per float4 of hidden units) sums
+// the p.splits partial tiles in slice order, forms the RMSNorm row factor from the partial sums
+// of squares, and applies the same epilogue math as direct_epilogue / qkv_epilogue
+template <int EPI>
+__global__ void __launch_bounds__(256) splitk_finish_kernel(GemmArgs p) {
+    const int nc = (EPI == EPI_SWIGLU ? p.N / 2 : p.N) / 4;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (idx >= (int64_t)p.M * nc) return;
+    const int row = (int)(idx / nc), c4 = (int)(idx - (int64_t)row * nc);
+    const int S = p.splits;
+    const int64_t MN = (int64_t)p.M * p.N;
+    float rs = 1.0f;
+    if (p.norm) {
+        float v = 0.f;
+        for (int k = 0; k < S; ++k) v += p.ws[S * MN + (int64_t)k * p.M + row];
+        rs = __builtin_amdgcn_rsqf(v * (1.0f / (float)p.K) + p.eps);
+    }
+    auto sum_at = [&](int col) {
+        const float* src = p.ws + (int64_t)row * p.N + col;
+        f32x4 v = *reinterpret_cast<const f32x4*>(src);
+        for (int k = 1; k < S; ++k) v += *reinterpret_cast<const f32x4*>(src + k * MN);
+        return v;
+    };
+    if constexpr (EPI == EPI_SWIGLU) {
+        // hidden units 16g + q: gate column 32g + q, up column 32g + 16 + q (fused W row groups)
+        const int hcol = 4 * c4, g = hcol >> 4, q = hcol & 15;
+        const f32x4 gt = sum_at(32 * g + q) * rs, up = sum_at(32 * g + 16 + q) * rs;
+        const f32x4 v = {silu_f(gt.x) * up.x, silu_f(gt.y) * up.y, silu_f(gt.z) * up.z, silu_f(gt.w) * up.w};
+        *reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + hcol) = v;
+    } else if constexpr (EPI == EPI_QKV) {
+        const int col = 4 * c4;
+        const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
+        const int sec = col < qdim ? 0 : (col < qdim + kvdim ? 1 : 2);
+        const int cc = col - (sec == 0 ? 0 : (sec == 1 ? qdim : qdim + kvdim));
+        const int head = cc / p.HD, d = cc - head * p.HD;
+        const int bidx = row / p.L, pos = start_of(p) + row - bidx * p.L;
+        const f32x4 v = sum_at(col) * (sec == 0 ? rs * p.q_scale : rs);
+        float2 c = {1.f, 1.f}, sn = {0.f, 0.f};
+        if (sec < 2) {
+            const int t = pos * (p.HD >> 1) + (d >> 1);
+            c = *reinterpret_cast<const float2*>(p.rope_cos + t);
+            sn = *reinterpret_cast<const float2*>(p.rope_sin + t);
+        }
+        const f32x4 r = {v.x * c.x - v.y * sn.x, v.x * sn.x + v.y * c.x,
+                         v.z * c.y - v.w * sn.y, v.z * sn.y + v.w * c.y};
+        float* base = sec == 0 ? p.q_out : (sec == 1 ? p.cache_k : p.cache_v);
+        const int64_t off = sec == 0 ? (int64_t)row * qdim + col
+                                     : (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d;
+        *reinterpret_cast<f32x4*>(base + off) = r;
+    } else {
+        const int col = 4 * c4;
+        f32x4 v = sum_at(col);
+        if constexpr (EPI == EPI_RESID) v += *reinterpret_cast<const f32x4*>(res_at(p, row, col));
+        else v *= rs;
+        *reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + col) = v;
+    }
+}
+
 // In-kernel clock stamps for diagnostic builds (never in the product path): shader-clock
 // counter and the 100 MHz real-time counter, read together.
 __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
@@ -202,8 +284,11 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// SPLIT: block b of a tiles x p.splits grid runs k-slice b / tiles of tile b % tiles (slice-major:
+// the blocks of one XCD share that slice of A in L2) and leaves its raw accumulators and partial
+// row sums of squares in p.ws (split_epilogue); splitk_finish_kernel sums the slices in order
 template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false,
-          int BK = 32, bool GLDS = true, int NS = 2>
+          int BK = 32, bool GLDS = true, int NS = 2, bool SPLIT = false>
 __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
     constexpr int BM = WM * TM * 16;
     constexpr int BN = WN * TN * 16;
@@ -222,8 +307,13 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     const int ntn = (p.N + BN - 1) / BN;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int tb = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntiles = SPLIT ? ((p.M + BM - 1) / BM) * ntn : 1;
+    const int ks = SPLIT ? tb / ntiles : 0;      // k-slice
+    const int t = SPLIT ? tb - ks * ntiles : tb;  // tile
     const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+    const int nk = SPLIT ? p.K / BK / p.splits : p.K / BK;  // k-tiles of this block
+    const int kb = ks * nk * BK;                           // its first k
     unsigned long long stamps[8];
     L3_STAMP(0);
 
@@ -336,7 +426,6 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     constexpr bool RES_PREFETCH = EPI == EPI_RESID && TM * TN <= 12;
     f32x4 res[RES_PREFETCH ? TM * TN : 1];
 
-    const int nk = p.K / BK;
     if constexpr (NS > 2) {
         // NS-deep LDS ring for latency-bound shapes (few blocks, weights streamed from HBM):
         // NS - 1 k-tiles in flight; counted vmcnt + raw s_barrier so the DMA spans barriers
@@ -367,7 +456,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         };
 #pragma unroll
         for (int i = 0; i < NS - 1; ++i)
-            if (i < nk) glds_tile(i, i * BK);
+            if (i < nk) glds_tile(i, kb + i * BK);
         for (int kt = 0; kt < nk; ++kt) {
             if (kt + NS - 2 < nk) wait_ring();
             else wait_vmcnt<0>();
@@ -375,7 +464,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             __builtin_amdgcn_sched_barrier(0);
-            if (kt + NS - 1 < nk) glds_tile((kt + NS - 1) % NS, (kt + NS - 1) * BK);
+            if (kt + NS - 1 < nk) glds_tile((kt + NS - 1) % NS, kb + (kt + NS - 1) * BK);
             if constexpr (RES_PREFETCH) {
                 if (kt == nk - 1) {
 #pragma unroll
@@ -393,9 +482,9 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         }
     } else {
     if constexpr (GLDS) {
-        glds_tile(0, 0);
+        glds_tile(0, kb);
     } else {
-        gload(0);
+        gload(kb);
         sstore(0);
     }
     __syncthreads();
@@ -403,10 +492,10 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     for (int kt = 0; kt < nk - 1; ++kt) {
         const int cur = kt & 1;
         if constexpr (GLDS) {
-            glds_tile(cur ^ 1, (kt + 1) * BK);  // lands while this tile computes
+            glds_tile(cur ^ 1, kb + (kt + 1) * BK);  // lands while this tile computes
             compute(cur);
         } else {
-            gload((kt + 1) * BK);
+            gload(kb + (kt + 1) * BK);
             compute(cur);
             sstore(cur ^ 1);
         }
@@ -429,6 +518,10 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     }
 
     // no barrier: each wave finishes its own tile from registers
+    if constexpr (SPLIT) {
+        split_epilogue<TM, TN>(p, acc, ss, ks, m0 + arow0, n0 + brow0, lane, wn == 0);
+        return;
+    }
     float rs[TM];
     const float inv_k = 1.0f / (float)p.K;
 #pragma unroll

@@ -52,6 +52,11 @@ struct GemmArgs {
     // EPI_STORE on the one-row GEMV (batch-1 lm_head): also the block's (value, index) argmax
     // over its columns -> amax_part[blockIdx.x], reduced by launch_argmax_parts
     ArgmaxPart* amax_part;
+    // Split-K (short M against a long K, gemm.hip launch_split): the caller's workspace of ws_cap
+    // floats (null: no split); the k-slices leave raw partial tiles [splits][M][N] and partial
+    // row sums of squares [splits][M] there, and splitk_finish_kernel applies the epilogue
+    float* ws; int64_t ws_cap;
+    int splits;                    // set by launch_gemm
 };
 constexpr int GEMV_MAXP = 8;
 constexpr int KV_BAK_SLOTS = 32;  // > the decode steps ever run ahead (runtime.hip SPEC_AHEAD)

@@ -109,6 +109,8 @@ struct l3_ctx {
     float *h = nullptr, *q = nullptr, *attn = nullptr, *hid = nullptr, *logits = nullptr;
     float* oparts = nullptr;         // [8, H, D] per-head O-proj rows of the fused decode attention
     float* hsum = nullptr;           // [8, D] h + those rows (gate|up writes it for down's residual)
+    float* skws = nullptr;           // split-K workspace of the layer GEMMs on `stream` (models
+    int64_t skws_cap = 0;            //   with D or FD >= 2048; gemm.hip launch_split), floats
     ArgmaxPart* amax_part = nullptr; // batch-1 lm_head's per-block argmax partials
     int amax_n = 0;                  // partials the last lm_head wrote (0: none, use the logits)
     int32_t *ids = nullptr, *amax = nullptr;
@@ -269,6 +271,10 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
         HIP_TRY(hipMalloc(&c->hsum, (int64_t)8 * D * 4));
     }
     HIP_TRY(hipMalloc(&c->amax_part, ((int64_t)c->d.vocab_size / 4 + 64) * sizeof(ArgmaxPart)));
+    if (!c->skws && (c->d.dim >= 2048 || c->d.hidden_dim >= 2048)) {
+        c->skws_cap = (int64_t)16 << 20;  // 64 MB: gate|up at M = 256 in 2 slices fits
+        HIP_TRY(hipMalloc(&c->skws, c->skws_cap * 4));
+    }
     c->ws_T = Tn;
     c->ws_B = Bn;
     return 0;
@@ -381,7 +387,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     }
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
-    dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum);
+    dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum); dfree(c->skws);
     dfree(c->amax); dfree(c->gather_ids);
     if (c->ids_pin) (void)hipHostFree(c->ids_pin);
     for (void* p : c->scratch) dfree(p);
@@ -594,6 +600,10 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     if (emb_ids) { g.A = c->emb; g.a_rows = emb_ids; }
     if (c->bak_capture) g.kv_bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD;
+    // split-K workspace: one, for the GEMMs on c->stream (a batch split's parts keep > 256 rows,
+    // past launch_split's range, so no two streams ever share it)
+    float* skws = s == c->stream ? c->skws : nullptr;
+    g.ws = skws; g.ws_cap = c->skws_cap;
     if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
     GemmArgs gu{};  // rmsnorm -> gate|up -> SwiGLU
     gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
@@ -602,6 +612,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     GemmArgs dn{};  // down + residual
     dn.A = hid; dn.lda = FD; dn.W = Ly.wd; dn.C = h; dn.ldc = D;
     dn.M = (int)T; dn.N = D; dn.K = FD; dn.norm = false;
+    gu.ws = dn.ws = skws; gu.ws_cap = dn.ws_cap = c->skws_cap;
     // Batch-1 decode: the O-proj rides in the attention launch as per-head partial rows, which
     // gate|up adds to its input and down to its residual (h + attn . Wo^T, llama3.py:211,253),
     // so a step runs one launch per layer fewer (device loop 0.104 -> 0.101 ms/step; at B = 8
@@ -628,6 +639,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
         GemmArgs o{};
         o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.C = h; o.ldc = D;
         o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
+        o.ws = skws; o.ws_cap = c->skws_cap;
         if (emb_ids) { o.res_src = c->emb; o.res_rows = emb_ids; }  // h = emb[ids] + attn . Wo^T
         if (timed_on(c, L3_K_OPROJ, s, [&] { return launch_gemm(EPI_RESID, o, s); })) return 1;
     }

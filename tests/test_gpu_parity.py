@@ -677,6 +677,39 @@ def test_c5_full_size_prefill_rows_match_oracle(c5_weights):
         assert _close(out[r:r + 1], ref(ids[r:r + 1], 0)) <= 1e-4
 
 
+@pytest.mark.timeout(900)
+def test_c5_short_rows_split_k_match_oracle(c5_weights):
+    """Short M against K >= 4096 (short prompts, batched decode at the Llama-3 shape) runs the
+    layer GEMMs split over K (gemm.hip launch_split: 16-, 64- and 128-row slice tiles, slices
+    summed in order by splitk_finish_kernel with each epilogue: QKV + RoPE + cache append,
+    SwiGLU, residual).  Prompts of 9..200 tokens at B = 1 and a 16-row batch of one-token
+    prompts, each against the oracle (f64, 1e-4) with the greedy id exact (llama3.py:163-211)."""
+    w, path = c5_weights
+    args1 = synth.llama3_shape(n_layers=2, max_batch_size=1)
+    ref = orc.OracleModel(w, args1)
+    m = llama3.Llama(path, args1, keep_host_weights=False)
+    rng = np.random.default_rng(33)
+    for L in (9, 24, 64, 100, 200):
+        ids = rng.integers(0, 128256, (1, L))
+        out = m(ids, 0)
+        want = ref(ids, 0)
+        assert np.isfinite(out).all()
+        assert _close(out, want) <= 1e-4, L
+        assert int(out[0, -1].argmax()) == int(want[0, -1].argmax())
+        # a decode step after the split-K prefill reads the cache rows its QKV finish wrote
+        nxt = np.array([[int(out[0, -1].argmax())]])
+        assert _close(m(nxt, L), ref(nxt, L)) <= 1e-4, L
+    del m
+    args16 = synth.llama3_shape(n_layers=2, max_batch_size=16)
+    m16 = llama3.Llama(path, args16, keep_host_weights=False)
+    ref16 = orc.OracleModel(w, args16)
+    ids = rng.integers(0, 128256, (16, 1))
+    out = m16(ids, 0)
+    want = ref16(ids, 0)
+    assert _close(out, want) <= 1e-4
+    np.testing.assert_array_equal(out[:, -1].argmax(-1), want[:, -1].argmax(-1))
+
+
 # ---- round 2: C4, lm_head ring cases, generate bounds, pinned host path ----------------------
 
 @pytest.mark.timeout(900)

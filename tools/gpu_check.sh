@@ -61,6 +61,13 @@ for s in "$@"; do
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
     c4) step c4 300 python bench.py --global-batch 2048 --steps 5 --warmup 1 --no-cpu-baseline --no-kernel-breakdown ;;
+    c5dec) step c5dec 600 python bench.py --workload c5decode --steps 30 ;;
+    c5decsk0) L3_SPLITK=0 step c5decsk0 600 python bench.py --workload c5decode --steps 30 ;;
+    c5decb*) L3_SPLITK_BLOCKS=${s#c5decb} step $s 600 python bench.py --workload c5decode --steps 30 ;;
+    c5deckt*) L3_SPLITK_MINKT=${s#c5deckt} step $s 600 python bench.py --workload c5decode --steps 30 ;;
+    c5deccfg[1-4]) L3_SPLITK_CFG=${s#c5deccfg} step $s 600 python bench.py --workload c5decode --steps 30 ;;
+    splitk) step splitk 900 python -u -m pytest tests/test_gpu_parity.py -k "c5_short or c5_slice_llama3" -x -v --timeout 900 --timeout-method thread ;;
+    c5decprof) L3_DECODE_GRAPH=0 step c5decprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/c5decprof -o run --output-format csv -- python bench.py --workload c5decode --steps 6 ;;
     c5small) step c5small 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     c5small1) L3_BATCH_SPLIT=1 step c5small1 600 python bench.py --workload c5 --layers 2 --steps 2 --warmup 1 ;;
     rccl) step rccl 180 python tools/rccl_selftest.py --world 2 --same-device ;;
