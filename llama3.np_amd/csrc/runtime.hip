@@ -285,7 +285,7 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 13;
+    if (minor) *minor = 14;
     return 0;
 }
 
