@@ -38,7 +38,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // are wrong with any bit set): 1 every tile full and unmasked for every block (no causal
 // structure), 2 p = s (no exp), 4 no K/V loads after tile 0, 8 no barrier in the tile loop,
 // 16 no softmax bookkeeping (no max / rescale / sum); 32 (timing study, results correct): K/V
-// tiles prefetched two ahead through two register sets
+// tiles prefetched two ahead through two register sets; 64 / 128 / 256 (timing study, results
+// correct): s_setprio(1) around both MFMA clusters / the score cluster / the P.V cluster
 template <int HD, int QBW, int G, int KT, int ABL = 0>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (G == 1 || G == 2 || G == 4), "shape");
@@ -156,6 +157,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 const int q_abs = start_pos + qblock_first + fq;
                 f32x4 sacc[KG];
                 bool live[KG];
+                if constexpr ((ABL & (64 | 128)) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int kg = 0; kg < KG; ++kg) {
                     live[kg] = !MASKED || (k0 + kg * 16) <= qmax_abs;     // wave-uniform
@@ -170,6 +172,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                         }
                     }
                 }
+                if constexpr ((ABL & (64 | 128)) != 0) __builtin_amdgcn_s_setprio(0);
                 // causal mask + tile max; lane holds keys k0 + kg*16 + fk + r for query q_abs
                 float mt = -INFINITY;
 #pragma unroll
@@ -205,6 +208,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
 #pragma unroll
                 for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;
                 }
+                if constexpr ((ABL & (64 | 256)) != 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int kg = 0; kg < KG; ++kg) {
                     if (!live[kg]) continue;
@@ -216,6 +220,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                             o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);
                         }
                 }
+                if constexpr ((ABL & (64 | 256)) != 0) __builtin_amdgcn_s_setprio(0);
             };
 #pragma unroll
             for (int j = 0; j < QBW; ++j) {

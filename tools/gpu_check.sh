@@ -37,6 +37,7 @@ for s in "$@"; do
     attnv2) step attnv2 300 tools/attn_tune 5 10 v2 ;;
     attnabl) step attnabl 300 tools/attn_tune 5 10 abl ;;
     attnpf2) step attnpf2 300 tools/attn_tune 5 10 pf2 ;;
+    attnprio) step attnprio 300 tools/attn_tune 5 10 prio ;;
     attnpipe) step attnpipe 300 tools/attn_tune 5 10 pipe ;;
     attnres) step attnres 300 tools/attn_tune 5 10 res ;;
     attnilv) step attnilv 300 tools/attn_tune 5 10 ilv ;;
