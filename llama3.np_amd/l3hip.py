@@ -176,6 +176,15 @@ class PinnedPool:
                 return
         lib().l3_host_free(addr)
 
+    def clear(self) -> None:
+        """Free every cached block (arrays still alive are freed when dropped)."""
+        with self._lock:
+            blocks = [a for v in self._free.values() for a in v]
+            self._free.clear()
+            self.keep = 0
+        for addr in blocks:
+            lib().l3_host_free(addr)
+
 
 pinned = PinnedPool()
 

@@ -34,6 +34,7 @@ from __future__ import annotations
 import os
 import sys
 import time
+import zipfile
 from typing import Iterator, Optional
 
 import numpy as np
@@ -41,7 +42,10 @@ import numpy as np
 import l3hip
 from config import ModelArgs
 from tokenizer import Tokenizer
-from utils import load_parameters
+from utils import StreamingNpz, load_parameters
+
+# A/B knob (tools/load_probe.py): L3_NPZ_PINNED=0 streams members through NpzFile instead
+_NPZ_PINNED = os.environ.get("L3_NPZ_PINNED", "1") != "0"
 
 DEFAULT_DEVICE = int(os.environ.get("LLAMA3_HIP_DEVICE", "0"))
 
@@ -267,7 +271,12 @@ class Llama:
         Llama-3-8B shape); the reference-style host attributes then hold placeholders."""
         self.args = args
         keep = keep_host_weights
-        weight = load_parameters(model_path)
+        pool = None
+        if keep or not _NPZ_PINNED or not zipfile.is_zipfile(model_path):
+            weight = load_parameters(model_path)
+        else:  # members read straight into page-locked buffers, uploaded by DMA, recycled
+            pool = l3hip.PinnedPool(keep=2)
+            weight = StreamingNpz(model_path, pool.empty)
         self.freqs_cos, self.freqs_sin = compute_cos_sin_cache(args.dim // args.n_heads,
                                                                args.max_seq_len)
         hidden = weight.get("model.layers.0.mlp.gate_proj.weight").shape[0]
@@ -280,14 +289,16 @@ class Llama:
         self.layers = [TransformerBlock(weight, i, args, _bind=(self._ctx, i), _keep_host=keep)
                        for i in range(args.n_layers)]
         norm_w = weight.get("model.norm.weight")
-        self.norm = RMSNorm(norm_w, eps=args.norm_eps)
+        self.norm = RMSNorm(norm_w if keep else np.array(norm_w), eps=args.norm_eps)
         self._ctx.upload(0, l3hip.W_FINAL_NORM, norm_w)
         lm = weight.get("lm_head.weight")
         self._ctx.upload(0, l3hip.W_LM_HEAD, lm)
         self.lm_head_weight = lm.T if keep else _Dropped(lm.shape[::-1])
         del lm
         self._ctx.finalize()
-        del weight
+        del weight, norm_w
+        if pool is not None:
+            pool.clear()
 
     @property
     def context(self) -> l3hip.Context:

@@ -1,0 +1,71 @@
+"""Streaming .npz reader (utils.StreamingNpz) against the reference's
+loader: ``utils.load_parameters`` is ``np.load`` (reference utils.py:4-5), so every member
+read by the fast path must equal ``np.load``'s array bit for bit, whatever the member's
+layout, and members the fast path does not take must come back through ``np.load``."""
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "llama3.np_amd"))
+import utils  # noqa: E402
+
+
+def _members(rng):
+    return {
+        "model.embed_tokens.weight": rng.standard_normal((97, 64), dtype=np.float32),
+        "model.norm.weight": rng.standard_normal(64, dtype=np.float32),
+        "scalar": np.float32(3.5),
+        "empty": np.zeros((0, 8), np.float32),
+        "f64": rng.standard_normal((5, 3)),                       # another dtype: fallback
+        "fortran": np.asfortranarray(rng.standard_normal((6, 4), dtype=np.float32)),
+        "big_endian": rng.standard_normal(7).astype(">f4"),      # not <f4: fallback
+    }
+
+
+@pytest.mark.parametrize("compressed", [False, True])
+def test_streaming_npz_equals_np_load(tmp_path, compressed):
+    path = str(tmp_path / "w.npz")
+    m = _members(np.random.default_rng(0))
+    (np.savez_compressed if compressed else np.savez)(path, **m)
+    ref = np.load(path, allow_pickle=False)
+    made = []
+
+    def alloc(shape, dtype):
+        a = np.empty(shape, dtype)
+        made.append(a)
+        return a
+
+    s = utils.StreamingNpz(path, alloc)
+    assert set(s.keys()) == set(ref.files)
+    for k in ref.files:
+        got, want = s.get(k), ref[k]
+        assert got.dtype == want.dtype and got.shape == want.shape, k
+        np.testing.assert_array_equal(got, want, err_msg=k)
+    assert s.get("missing") is None and s.get("missing", 7) == 7
+    assert "model.norm.weight" in s
+    with pytest.raises(KeyError):
+        s["missing"]
+    # stored members of the fast-path layout land in the caller's buffers; compressed ones never
+    assert len(made) == (0 if compressed else 4)
+    s.close()
+
+
+def test_streaming_npz_detects_truncation(tmp_path):
+    path = str(tmp_path / "w.npz")
+    np.savez(path, a=np.arange(4096, dtype=np.float32))
+    with open(path, "rb") as f:
+        blob = f.read()
+    cut = str(tmp_path / "cut.npz")
+    # keep the central directory (so the zip opens) but lose data bytes of the member
+    import zipfile
+
+    zi = zipfile.ZipFile(path).getinfo("a.npy")
+    data_end = zi.header_offset + 30 + len(zi.filename) + len(zi.extra) + zi.file_size
+    with open(cut, "wb") as f:
+        f.write(blob[: data_end - 1000] + blob[data_end:])
+    s = utils.StreamingNpz(cut, lambda shape, dtype: np.empty(shape, dtype))
+    with pytest.raises((ValueError, OSError)):
+        s.get("a")

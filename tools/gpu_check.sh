@@ -89,6 +89,7 @@ for s in "$@"; do
     pmcgemm) step pmcgemmA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcgemmA -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1
              step pmcgemmB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcgemmB -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 ;;
     attnprof) step attnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attnprof -o run --output-format csv -- tools/attn_tune 3 10 ;;
+    loadprobe) step loadprobe 600 python tools/load_probe.py ;;
     cabi) step cabi 300 python -u -m pytest tests/test_c_abi_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
