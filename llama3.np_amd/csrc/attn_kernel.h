@@ -40,14 +40,29 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // 16 no softmax bookkeeping (no max / rescale / sum); 32 (timing study, results correct): K/V
 // tiles prefetched two ahead through two register sets; 64 / 128 / 256 (timing study, results
 // correct): s_setprio(1) around both MFMA clusters / the score cluster / the P.V cluster
-template <int HD, int QBW, int G, int KT, int ABL = 0>
+//
+// DEFER (HD 48): three K/V slots instead of two, and the diagonal (masked) units of the even
+// q-block slots j (C3: the even tiles' diagonal units) run one barrier interval later, first
+// thing after the next tile's barrier (the tile is still in its slot then; the store of tile
+// t+1 goes to the slot of t-2).
+// A q-block's units still run in tile order, so the output is bit-identical.  Why: with the
+// zig-zag deal the busiest wave carries 16 / 12 / 8 / 4 key groups between the four barriers of
+// C3 against 34 of work per wave (the diagonal unit of q-block 4t+r costs r+1 groups, and the
+// wave holding r = 3 alternates); deferring the even tiles' diagonal units pairs r with 3 - r,
+// so every wave carries 12 / 13 / 4 / 5.  The third slot fits beside a second workgroup per CU
+// only with an unpadded K image: rows of 48 floats, float4 quad q of row r stored at
+// q ^ 3*((r>>3)&1), which keeps the 16-lane ds_read_b128 groups of the score reads on 16
+// distinct bank quads (25 KB per slot, 75 KB in all).
+template <int HD, int QBW, int G, int KT, int ABL = 0, bool DEFER = false>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (G == 1 || G == 2 || G == 4), "shape");
+    static_assert(!DEFER || (HD == 48 && (ABL & 32) == 0), "DEFER: the swizzled K image is laid out for HD 48");
+    constexpr int NS = DEFER ? 3 : 2;         // K/V slots
     constexpr int WPH = 4 / G;                // waves per head
     constexpr int NQB = QBW * WPH;            // 16-query blocks per head per workgroup
     constexpr int QW = 16 * NQB;              // queries per workgroup
     constexpr int ND = HD / 16;               // 16-wide d groups
-    constexpr int KSTR = HD + 8;              // == 8 mod 16 floats
+    constexpr int KSTR = DEFER ? HD : HD + 8; // padded: == 8 mod 16 floats; DEFER: swizzled
     // P.V reads V[key = kg*16 + 4(lane>>4) + s][d = dg*16 + (lane&15)] with ds_read_b32: lanes
     // 0-15 and 16-31 (one bank group) are 4 rows apart, so 4*VSTR must be == 16 (mod 32):
     // VSTR == 4 (mod 8) puts the two 16-lane halves on disjoint banks (HD is a multiple of 16)
@@ -56,8 +71,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     constexpr int K_IT = (K_F4 + 255) / 256;
     constexpr int KG = KT / 16;               // 16-key groups per tile
 
-    __shared__ __attribute__((aligned(16))) float Ks[2][KT][KSTR];
-    __shared__ __attribute__((aligned(16))) float Vs[2][KT][VSTR];
+    __shared__ __attribute__((aligned(16))) float Ks[NS][KT][KSTR];
+    __shared__ __attribute__((aligned(16))) float Vs[NS][KT][VSTR];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = wid % G, part = wid / G;
@@ -67,6 +82,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     const int qdim = p.H * HD;
     const int fq = lane & 15;       // query within a 16-block
     const int fk = 4 * (lane >> 4); // k offset of this lane's operand quad
+    // column of this lane's K fragment quad within a 16-wide d group (DEFER: swizzled image;
+    // the row's bit 3 is fq's, so the swizzle is a per-lane constant)
+    const int fkx = DEFER ? 4 * ((lane >> 4) ^ (3 * ((fq >> 3) & 1))) : fk;
 
     // this wave's q blocks (zig-zag over the WPH waves of its head)
     int qblk[QBW];
@@ -121,7 +139,8 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             const int f = tid + 256 * i;
             if (K_F4 % 256 == 0 || f < K_F4) {
                 const int row = f / (HD / 4), c = (f % (HD / 4)) * 4;
-                *reinterpret_cast<f32x4*>(&Ks[buf][row][c]) = sk[i];
+                const int ck = DEFER ? (c ^ (12 * ((row >> 3) & 1))) : c;  // quad ^ 3 on rows 8-15 of 16
+                *reinterpret_cast<f32x4*>(&Ks[buf][row][ck]) = sk[i];
                 *reinterpret_cast<f32x4*>(&Vs[buf][row][c]) = sv[i];
             }
         }
@@ -135,8 +154,9 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
         if (ntiles > 1) gload(1);  // set A holds tile 1
     }
     __syncthreads();
+    int cur = 0;  // slot of this tile (tile % NS)
     for (int tile = 0; tile < ntiles; ++tile) {
-        const int cur = tile & 1;
+        const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
         if constexpr ((ABL & 32) != 0) {  // tile + 2 into the set that held tile (its store is done)
             if (tile + 2 < ntiles) {
                 if (tile & 1) gload_into(tile + 2, rk, rv);
@@ -152,7 +172,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             // unmasked body has no wave-uniform branches, so hipcc can interleave the four
             // key groups' S chains and hoist the V reads
             auto qblock_tile = [&](const int j, const int qblock_first, const int qmax_abs,
-                                   auto masked_tag) {
+                                   const int cur, const int k0, auto masked_tag) {
                 constexpr bool MASKED = decltype(masked_tag)::value;
                 const int q_abs = start_pos + qblock_first + fq;
                 f32x4 sacc[KG];
@@ -165,7 +185,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                     if (live[kg]) {
 #pragma unroll
                         for (int dg = 0; dg < ND; ++dg) {
-                            const f32x4 kf = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
+                            const f32x4 kf = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fkx]);
 #pragma unroll
                             for (int s = 0; s < 4; ++s)
                                 sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
@@ -222,6 +242,24 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 }
                 if constexpr ((ABL & (64 | 256)) != 0) __builtin_amdgcn_s_setprio(0);
             };
+            if constexpr (DEFER) {
+                if (tile > 0) {  // the even q-block slots' diagonal units of tile - 1, deferred
+                    const int pk0 = k0 - KT, prv = (cur == 0) ? NS - 1 : cur - 1;
+#pragma unroll
+                    for (int j = 0; j < QBW; j += 2) {
+                        const int qblock_first = q_lo + qblk[j] * 16;
+                        if (qblock_first >= p.L) continue;
+                        const int qmax_abs = start_pos + min(qblock_first + 15, p.L - 1);
+                        if (pk0 > qmax_abs || pk0 + KT - 1 <= start_pos + qblock_first) continue;
+                        qblock_tile(j, qblock_first, qmax_abs, prv, pk0, std::integral_constant<bool, true>{});
+                    }
+                }
+            }
+            // DEFER: the diagonal units of the even q-block slots j wait for the next interval
+            // (never the last tile's).  With the zig-zag deal at start_pos 0 and one workgroup per
+            // 256 queries (C3), slot j's diagonal tile is tile j, so this defers the even tiles'
+            // diagonal units; any other shape stays correct, only the balance differs
+            const bool defer_even = DEFER && tile + 1 < ntiles;
 #pragma unroll
             for (int j = 0; j < QBW; ++j) {
                 const int qblock_first = q_lo + qblk[j] * 16;
@@ -230,20 +268,21 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 if (!(ABL & 1) && k0 > qmax_abs) continue;                // whole tile masked
                 // every key of the tile <= every query of the block: no mask, all groups live
                 if ((ABL & 1) || k0 + KT - 1 <= start_pos + qblock_first)
-                    qblock_tile(j, qblock_first, qmax_abs, std::integral_constant<bool, false>{});
-                else
-                    qblock_tile(j, qblock_first, qmax_abs, std::integral_constant<bool, true>{});
+                    qblock_tile(j, qblock_first, qmax_abs, cur, k0, std::integral_constant<bool, false>{});
+                else if (!(defer_even && (j & 1) == 0))
+                    qblock_tile(j, qblock_first, qmax_abs, cur, k0, std::integral_constant<bool, true>{});
             }
         }
         if constexpr ((ABL & 32) != 0) {
             if (tile + 1 < ntiles) {
-                if (tile & 1) sstore_from(cur ^ 1, rk2, rv2);
-                else sstore_from(cur ^ 1, rk, rv);
+                if (tile & 1) sstore_from(nxt, rk2, rv2);
+                else sstore_from(nxt, rk, rv);
             }
         } else if (!(ABL & 4) && tile + 1 < ntiles) {
-            sstore(cur ^ 1);
+            sstore(nxt);
         }
         if constexpr (!(ABL & 8)) __syncthreads();
+        cur = nxt;
     }
 
     // finalize: l = sum over the 4 lane groups; lane holds O^T[d = dg*16 + fk + r][q = fq]

@@ -13,6 +13,7 @@ uses it to fail early on a missing tensor instead of the reference's late
 ``AttributeError`` on ``None.T`` (``llama3.py:133-136``).
 """
 
+import os
 import struct
 import zipfile
 from typing import Callable, List, Optional
@@ -30,17 +31,21 @@ class StreamingNpz:
     ``get(name)`` reads one member straight from the file into a buffer made by
     ``alloc(shape, dtype)`` — page-locked memory from ``l3hip.PinnedPool`` in
     ``Llama(..., keep_host_weights=False)`` — so the H2D upload that follows is a DMA, and
-    the bytes are copied once (page cache -> pinned buffer by one ``readinto``) instead of
-    three times (``NpzFile``: zip stream -> 256 KB chunks -> array, with a CRC-32 pass, then
-    the runtime's pageable bounce).  Stored (uncompressed, as ``np.savez`` writes them)
-    little-endian fp32 C-order members take this path; any other member (compressed,
+    the bytes are copied once (page cache -> pinned buffer, 32 MB ``preadv`` pieces on
+    ``threads`` threads at once) instead of three times (``NpzFile``: zip stream -> 256 KB
+    chunks -> array, with a CRC-32 pass, then the runtime's pageable bounce).  Stored
+    (uncompressed, as ``np.savez`` writes them) little-endian fp32 C-order members take this path; any other member (compressed,
     Fortran order, another dtype, a newer ``.npy`` header) is read by ``NpzFile`` as the
     reference's ``load_parameters`` would (same values either way; the fast path skips the
     zip CRC check, the ``.npy`` header is still parsed and checked against the member size).
     Same lookup contract as the reference's mapping: ``get`` returns ``default`` for a
     missing key."""
 
-    def __init__(self, model_path, alloc: Callable[[tuple, np.dtype], np.ndarray]):
+    CHUNK = 32 << 20  # bytes per read request
+
+    def __init__(self, model_path, alloc: Callable[[tuple, np.dtype], np.ndarray],
+                 threads: int = 8):
+        self.threads = max(1, min(threads, os.cpu_count() or 1))
         self._alloc = alloc
         self._zip = zipfile.ZipFile(model_path)
         self._raw = open(model_path, "rb", buffering=0)
@@ -48,6 +53,7 @@ class StreamingNpz:
                          if zi.filename.endswith(".npy")}
         self._npz: Optional[np.lib.npyio.NpzFile] = None
         self._path = model_path
+        self._pool = None
 
     def keys(self):
         return self._members.keys()
@@ -94,15 +100,33 @@ class StreamingNpz:
             raise ValueError(f"{self._path}: member {zi.filename!r} size does not match its header")
         out = self._alloc(tuple(shape), np.float32)
         view = memoryview(out.reshape(-1)).cast("B")
-        got = 0
-        while got < nbytes:
-            n = f.readinto(view[got:])
-            if not n:
-                raise ValueError(f"{self._path}: member {zi.filename!r} truncated")
-            got += n
+        data = f.tell()
+        chunks = [(o, min(nbytes, o + self.CHUNK)) for o in range(0, nbytes, self.CHUNK)]
+        if len(chunks) > 1 and self.threads > 1:
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._pool = ThreadPoolExecutor(self.threads)
+            list(self._pool.map(lambda c: self._pread(view, data, *c, zi), chunks))
+        else:
+            for c in chunks:
+                self._pread(view, data, *c, zi)
         return out
 
+    def _pread(self, view, data, lo, hi, zi):
+        # os.preadv releases the GIL: chunks of one member are copied out of the page cache by
+        # several threads at once (one thread tops out near 4.4 GB/s on the box)
+        fd = self._raw.fileno()
+        while lo < hi:
+            n = os.preadv(fd, [view[lo:hi]], data + lo)
+            if not n:
+                raise ValueError(f"{self._path}: member {zi.filename!r} truncated")
+            lo += n
+
     def close(self) -> None:
+        if self._pool is not None:
+            self._pool.shutdown()
+            self._pool = None
         self._raw.close()
         self._zip.close()
         if self._npz is not None:

@@ -69,3 +69,15 @@ def test_streaming_npz_detects_truncation(tmp_path):
     s = utils.StreamingNpz(cut, lambda shape, dtype: np.empty(shape, dtype))
     with pytest.raises((ValueError, OSError)):
         s.get("a")
+
+
+def test_streaming_npz_threaded_pieces(tmp_path):
+    """A member larger than one read piece is copied by several threads; every byte lands."""
+    path = str(tmp_path / "w.npz")
+    a = np.random.default_rng(3).standard_normal((301, 257), dtype=np.float32)
+    np.savez(path, a=a, b=a[:7])
+    s = utils.StreamingNpz(path, lambda shape, dtype: np.empty(shape, dtype), threads=4)
+    s.CHUNK = 4096 + 12  # pieces not aligned to rows or pages
+    np.testing.assert_array_equal(s.get("a"), a)
+    np.testing.assert_array_equal(s["b"], a[:7])
+    s.close()

@@ -46,6 +46,13 @@ struct Variant {
                 hipLaunchKernelGGL((attn_fwd_v2_kernel<HD, QBW, G, KT, WPE>), grid, dim3(256), 0, s, a); \
             }}
 
+#define ADEF(HD, QBW, G, KT)                                                                  \
+    Variant{"defer<" #HD ",q" #QBW ",g" #G ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * (4 / G);                                        \
+                dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
+                hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT, 0, true>), grid, dim3(256), 0, s, a); \
+            }}
+
 #define AABL(ABL)                                                                             \
     Variant{"v1<48,q4,kt64> abl" #ABL, [](const AttnArgs& a, hipStream_t s) {                  \
                 dim3 grid((a.L + 255) / 256, a.H, a.B);                                        \
@@ -155,6 +162,16 @@ int main(int argc, char** argv) {
     if (argc > 3 && std::string(argv[3]) == "pf2") {
         run("stories15M C3", 256, 256, 6, 6, 48, {AVAR(48, 4, 1, 64), AABL(32)}, rounds, iters);
         run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, {AVAR(48, 4, 1, 64), AABL(32)}, 1, 1, 37);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "defer") {  // 3 slots, even tiles' diagonal units deferred
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), ADEF(48, 4, 1, 64), AVAR(48, 4, 1, 64), ADEF(48, 4, 1, 64)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        run("stories15M L=100", 16, 100, 6, 6, 48, {AVAR(48, 4, 1, 64), ADEF(48, 4, 1, 64)}, 1, 1);
+        run("stories15M L=333 at 5", 4, 333, 6, 6, 48, {AVAR(48, 4, 1, 64), ADEF(48, 4, 1, 64)}, 1, 1, 5);
+        run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48, {AVAR(48, 4, 2, 64), ADEF(48, 4, 2, 64)}, 1, 1, 19);
+        run("GQA n_rep 4, L=300 at 3", 2, 300, 8, 2, 48, {AVAR(48, 4, 4, 64), ADEF(48, 4, 4, 64)}, 1, 1, 3);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "ring") {  // LDS-DMA ring variants against v1

@@ -22,6 +22,7 @@ for s in "$@"; do
     testsx) step tests 1200 python -m pytest tests -m gpu -q -x -rf --timeout 600 ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --no-cpu-baseline ;;
+    defer[01]) L3_ATTN_DEFER=${s#defer} step $s 300 python bench.py --no-cpu-baseline ;;
     split[1-4]) L3_BATCH_SPLIT=${s#split} step $s 300 python bench.py --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1
@@ -42,6 +43,7 @@ for s in "$@"; do
     attnres) step attnres 300 tools/attn_tune 5 10 res ;;
     attnilv) step attnilv 300 tools/attn_tune 5 10 ilv ;;
     attnv3) step attnv3 300 tools/attn_tune 5 10 v3 ;;
+    attndefer) step attndefer 300 tools/attn_tune 5 10 defer ;;
     attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
     floor) step floor 120 tools/launch_floor ;;
