@@ -68,14 +68,21 @@ static hipError_t launch_split(int epi, const GemmArgs& a, hipStream_t s) {
     }
 }
 
-template <int EPI, int MR, int LPU, bool PARTS = false>
+template <int EPI, int MR, int LPU, bool PARTS = false, bool NT = false>
 static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
     const int units = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? a.N / 2 : a.N;
     const int per_block = 4 * (64 / LPU);
     const dim3 grid((unsigned)((units + per_block - 1) / per_block), (unsigned)((a.M + MR - 1) / MR)),
         block(256);
-    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU, PARTS>), grid, block, MR == 1 ? 0 : (size_t)MR * a.K * 4, s, a);
+    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU, PARTS, NT>), grid, block, MR == 1 ? 0 : (size_t)MR * a.K * 4, s, a);
     return hipGetLastError();
+}
+
+// non-temporal W loads for the one-row GEMV over a weight larger than the caches would keep
+// (>= 64 MB: the Llama-3-shape decode; gemv_kernel NT); L3_GEMV_NT=0 turns them off (A/B)
+static bool gemv_nt(const GemmArgs& a) {
+    static const int on = [] { const char* e = getenv("L3_GEMV_NT"); return e ? atoi(e) : 1; }();
+    return on && (int64_t)a.N * a.K * 4 >= ((int64_t)64 << 20);
 }
 
 // the O-proj partial rows of the fused decode attention (GemmArgs::parts): EPI_SWIGLU carries
@@ -86,12 +93,12 @@ static hipError_t launch_gemv_parts(const GemmArgs& a, hipStream_t s) {
     const int k4 = a.K / 4;
     if constexpr (EPI == EPI_SWIGLU) {
         if (k4 <= 128) return launch_gemv_lpu<EPI, 1, 32, true>(a, s);
-        return launch_gemv_lpu<EPI, 1, 64, true>(a, s);
     } else {
         if (k4 <= 128) return launch_gemv_lpu<EPI, 1, 16, true>(a, s);
         if (k4 <= 256) return launch_gemv_lpu<EPI, 1, 32, true>(a, s);
-        return launch_gemv_lpu<EPI, 1, 64, true>(a, s);
     }
+    if (gemv_nt(a)) return launch_gemv_lpu<EPI, 1, 64, true, true>(a, s);
+    return launch_gemv_lpu<EPI, 1, 64, true>(a, s);
 }
 
 // lanes per unit from K: ~5-8 float4 per lane per W row in one chunk at the stories15M sizes;
@@ -105,6 +112,9 @@ static int gemv_lpu(const GemmArgs& a) {
 
 template <int EPI, int MR>
 static hipError_t launch_gemv_mr(const GemmArgs& a, hipStream_t s) {
+    if constexpr (MR == 1) {
+        if (gemv_lpu(a) == 64 && gemv_nt(a)) return launch_gemv_lpu<EPI, 1, 64, false, true>(a, s);
+    }
     switch (gemv_lpu(a)) {
         case 16: return launch_gemv_lpu<EPI, MR, 16>(a, s);
         case 32: return launch_gemv_lpu<EPI, MR, 32>(a, s);

@@ -564,7 +564,12 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 // FFN's input, llama3.py:253), EPI_RESID to its residual (the down-proj's residual is that same
 // row, :259), always in head order.  Their loads join the same round trip (GEMV_MAXP per
 // piece, predicated past nparts, so CH drops to 4).
-template <int EPI, int MR, int LPU, bool PARTS = false>
+//
+// NT: the W pieces are loaded non-temporal (global_load ... nt): weights that one wave streams
+// once per call and that do not fit the caches anyway (Llama-3-shape decode: 67 MB - 2.1 GB per
+// launch); the small layer weights of stories15M stay on the default policy (they are re-read
+// from the caches every step).
+template <int EPI, int MR, int LPU, bool PARTS = false, bool NT = false>
 __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     extern __shared__ __attribute__((aligned(16))) float xs[];  // [MR][K]
     static_assert(!PARTS || MR == 1, "partial rows only on the one-row GEMV");
@@ -607,7 +612,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             const int k4 = j + LPU * (t0 + t);
 #pragma unroll
             for (int r = 0; r < ROWS; ++r)
-                w[r][t] = k4 < K4 ? W4[(int64_t)wrow[r] * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
+                w[r][t] = k4 >= K4 ? f32x4{0.f, 0.f, 0.f, 0.f}
+                          : NT ? __builtin_nontemporal_load(&W4[(int64_t)wrow[r] * K4 + k4])
+                               : W4[(int64_t)wrow[r] * K4 + k4];
             if constexpr (DIRECT) xv[t] = X4[min(k4, K4 - 1)];
             if constexpr (XPARTS) {
 #pragma unroll
