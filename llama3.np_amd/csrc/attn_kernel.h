@@ -53,17 +53,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // only with an unpadded K image: rows of 48 floats, float4 quad q of row r stored at
 // q ^ 3*((r>>3)&1), which keeps the 16-lane ds_read_b128 groups of the score reads on 16
 // distinct bank quads (25 KB per slot, 75 KB in all).
-//
-// SPEC (C3: L = 256 from position 0, one workgroup per (batch, head)): the tile loop is unrolled
-// and each wave's work per tile is known at compile time — with the zig-zag deal q-block slot j
-// has its diagonal in tile j, so tile t runs slot t masked and slots t+1.. unmasked, no branch
-// between units — which leaves hipcc free to overlap one unit's softmax with another's MFMAs.
-// Same units in the same order per q-block: bit-identical output.
-template <int HD, int QBW, int G, int KT, int ABL = 0, bool DEFER = false, int SPEC = 0>
+template <int HD, int QBW, int G, int KT, int ABL = 0, bool DEFER = false>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (G == 1 || G == 2 || G == 4), "shape");
     static_assert(!DEFER || (HD == 48 && (ABL & 32) == 0), "DEFER: the swizzled K image is laid out for HD 48");
-    static_assert(!SPEC || (QBW == 4 && G == 1 && KT == 64 && !DEFER && ABL == 0), "SPEC: the C3 kernel");
     constexpr int NS = DEFER ? 3 : 2;         // K/V slots
     constexpr int WPH = 4 / G;                // waves per head
     constexpr int NQB = QBW * WPH;            // 16-query blocks per head per workgroup
@@ -103,7 +96,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     const int q_lo = qt * QW;
     const int q_hi = min(p.L, q_lo + QW);
     const int key_end = start_pos + q_hi;  // keys [0, key_end) are needed
-    const int ntiles = SPEC ? 4 : (key_end + KT - 1) / KT;
+    const int ntiles = (key_end + KT - 1) / KT;
 
     f32x4 qreg[QBW][ND];
     f32x4 o[QBW][ND];
@@ -249,29 +242,6 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
                 }
                 if constexpr ((ABL & (64 | 256)) != 0) __builtin_amdgcn_s_setprio(0);
             };
-            if constexpr (SPEC) {  // slot j: skipped below tile j, masked at tile j, full above
-                auto spec_tile = [&](auto tile_tag) {
-                    constexpr int T = decltype(tile_tag)::value;
-#pragma unroll
-                    for (int j = T; j < QBW; ++j) {
-                        const int qblock_first = qblk[j] * 16;
-                        // SPEC 2: nothing crosses a unit boundary; 3: ALU, VALU, MFMA and
-                        // transcendental work may (no memory): adjacent units overlap their math
-                        if constexpr (SPEC == 2) __builtin_amdgcn_sched_barrier(0);
-                        if constexpr (SPEC == 3) __builtin_amdgcn_sched_barrier(0x040B);
-                        if (j == T)
-                            qblock_tile(j, qblock_first, qblock_first + 15, cur, k0, std::integral_constant<bool, true>{});
-                        else
-                            qblock_tile(j, qblock_first, qblock_first + 15, cur, k0, std::integral_constant<bool, false>{});
-                    }
-                };
-                switch (tile) {
-                    case 0: spec_tile(std::integral_constant<int, 0>{}); break;
-                    case 1: spec_tile(std::integral_constant<int, 1>{}); break;
-                    case 2: spec_tile(std::integral_constant<int, 2>{}); break;
-                    default: spec_tile(std::integral_constant<int, 3>{}); break;
-                }
-            }
             if constexpr (DEFER) {
                 if (tile > 0) {  // the even q-block slots' diagonal units of tile - 1, deferred
                     const int pk0 = k0 - KT, prv = (cur == 0) ? NS - 1 : cur - 1;
@@ -291,7 +261,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             // diagonal units; any other shape stays correct, only the balance differs
             const bool defer_even = DEFER && tile + 1 < ntiles;
 #pragma unroll
-            for (int j = 0; j < (SPEC ? 0 : QBW); ++j) {
+            for (int j = 0; j < QBW; ++j) {
                 const int qblock_first = q_lo + qblk[j] * 16;
                 if (qblock_first >= p.L) continue;                        // padding block
                 const int qmax_abs = start_pos + min(qblock_first + 15, p.L - 1);

@@ -53,12 +53,6 @@ struct Variant {
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT, 0, true>), grid, dim3(256), 0, s, a); \
             }}
 
-#define ASPEC(M)                                                                              \
-    Variant{"spec" #M "<48,q4,g1,kt64>", [](const AttnArgs& a, hipStream_t s) {                \
-                dim3 grid(1, a.H, a.B);                                                       \
-                hipLaunchKernelGGL((attn_fwd_kernel<48, 4, 1, 64, 0, false, M>), grid, dim3(256), 0, s, a); \
-            }}
-
 #define AABL(ABL)                                                                             \
     Variant{"v1<48,q4,kt64> abl" #ABL, [](const AttnArgs& a, hipStream_t s) {                  \
                 dim3 grid((a.L + 255) / 256, a.H, a.B);                                        \
@@ -178,12 +172,6 @@ int main(int argc, char** argv) {
         run("stories15M L=333 at 5", 4, 333, 6, 6, 48, {AVAR(48, 4, 1, 64), ADEF(48, 4, 1, 64)}, 1, 1, 5);
         run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48, {AVAR(48, 4, 2, 64), ADEF(48, 4, 2, 64)}, 1, 1, 19);
         run("GQA n_rep 4, L=300 at 3", 2, 300, 8, 2, 48, {AVAR(48, 4, 4, 64), ADEF(48, 4, 4, 64)}, 1, 1, 3);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "spec") {  // C3-specialised: tile loop unrolled, units known
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), ASPEC(1), ASPEC(2), ASPEC(3), AVAR(48, 4, 1, 64), ASPEC(1), ASPEC(2), ASPEC(3)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M C3 B=128", 128, 256, 6, 6, 48, v, rounds, iters);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "ring") {  // LDS-DMA ring variants against v1

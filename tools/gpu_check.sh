@@ -44,7 +44,6 @@ for s in "$@"; do
     attnilv) step attnilv 300 tools/attn_tune 5 10 ilv ;;
     attnv3) step attnv3 300 tools/attn_tune 5 10 v3 ;;
     attndefer) step attndefer 300 tools/attn_tune 5 10 defer ;;
-    attnspec) step attnspec 300 tools/attn_tune 5 10 spec ;;
     attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
     floor) step floor 120 tools/launch_floor ;;
