@@ -754,6 +754,18 @@ def test_lm_head_ring_integer_exact(ctx, M):
     np.testing.assert_array_equal(ctx.op_linear(x, w), x @ w.T)
 
 
+@pytest.mark.parametrize("K,N", [(4096, 4100), (4096, 4096), (288, 32000)])
+def test_one_row_gemv_integer_exact(ctx, K, N):
+    """The one-row GEMV (batch-1 decode, llama3.py:166-178,211,304-307 at M = 1) on integer
+    operands: the first two weights are >= 64 MB and take the non-temporal W loads
+    (gemv_kernel NT, the Llama-3-shape decode), the last (the stories15M lm_head, 37 MB) the
+    default policy; both bit-exact."""
+    rng = np.random.default_rng(K + N)
+    x = rng.integers(-4, 5, (1, K)).astype(np.float32)
+    w = rng.integers(-4, 5, (N, K)).astype(np.float32)
+    np.testing.assert_array_equal(ctx.op_linear(x, w), x @ w.T)
+
+
 def test_generate_all_bounds_at_max_seq_len(tmpdir_mod):
     """The device loop's last decode step runs at position max_new_tokens - 1: max_new_tokens
     == max_seq_len is the longest legal run (ids equal the oracle's, the last step writing the
