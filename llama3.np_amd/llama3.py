@@ -275,7 +275,7 @@ class Llama:
         if keep or not _NPZ_PINNED or not zipfile.is_zipfile(model_path):
             weight = load_parameters(model_path)
         else:  # members read straight into page-locked buffers, uploaded by DMA, recycled
-            pool = l3hip.PinnedPool(keep=2)
+            pool = l3hip.PinnedPool(keep=3)  # gate, up and down share a size and live together
             weight = StreamingNpz(model_path, pool.empty)
         self.freqs_cos, self.freqs_sin = compute_cos_sin_cache(args.dim // args.n_heads,
                                                                args.max_seq_len)
