@@ -42,10 +42,12 @@ import numpy as np
 import l3hip
 from config import ModelArgs
 from tokenizer import Tokenizer
-from utils import StreamingNpz, load_parameters
+from utils import RecyclingAlloc, StreamingNpz, load_parameters
 
-# A/B knob (tools/load_probe.py): L3_NPZ_PINNED=0 streams members through NpzFile instead
-_NPZ_PINNED = os.environ.get("L3_NPZ_PINNED", "1") != "0"
+# .npz reader (A/B: tools/load_probe.py): "threads" — utils.StreamingNpz into ordinary arrays,
+# recycled when host copies are not kept (default), "pinned" — into recycled page-locked buffers
+# when host copies are not kept, "npzfile" — NumPy's NpzFile as the reference's load_parameters
+_NPZ_READER = os.environ.get("L3_NPZ_READER", "threads")
 
 DEFAULT_DEVICE = int(os.environ.get("LLAMA3_HIP_DEVICE", "0"))
 
@@ -272,11 +274,14 @@ class Llama:
         self.args = args
         keep = keep_host_weights
         pool = None
-        if keep or not _NPZ_PINNED or not zipfile.is_zipfile(model_path):
+        if _NPZ_READER == "npzfile" or not zipfile.is_zipfile(model_path):
             weight = load_parameters(model_path)
-        else:  # members read straight into page-locked buffers, uploaded by DMA, recycled
-            pool = l3hip.PinnedPool(keep=3)  # gate, up and down share a size and live together
-            weight = StreamingNpz(model_path, pool.empty)
+        elif keep:  # the arrays NpzFile would give, read by 8 threads without the zip CRC pass
+            weight = StreamingNpz(model_path, np.empty)
+        else:  # streaming: each member's buffer recycled once uploaded (gate, up and down of a
+            # layer share a size and live together: 3 per size)
+            pool = l3hip.PinnedPool(keep=3) if _NPZ_READER == "pinned" else RecyclingAlloc(keep=3)
+            weight = StreamingNpz(model_path, pool.empty if _NPZ_READER == "pinned" else pool)
         self.freqs_cos, self.freqs_sin = compute_cos_sin_cache(args.dim // args.n_heads,
                                                                args.max_seq_len)
         hidden = weight.get("model.layers.0.mlp.gate_proj.weight").shape[0]

@@ -13,6 +13,7 @@ uses it to fail early on a missing tensor instead of the reference's late
 ``AttributeError`` on ``None.T`` (``llama3.py:133-136``).
 """
 
+import ctypes
 import os
 import struct
 import zipfile
@@ -137,6 +138,46 @@ class StreamingNpz:
             self.close()
         except Exception:
             pass
+
+
+class RecyclingAlloc:
+    """``alloc(shape, dtype)`` for ``StreamingNpz`` when the arrays are dropped after upload
+    (``keep_host_weights=False``): an array's memory goes back to a per-size free list once the
+    array and every view of it are gone, and the next member of that size reuses it — no fresh
+    pages to fault in and no unmap per member (at most ``keep`` blocks per size are kept)."""
+
+    def __init__(self, keep: int = 3):
+        import threading
+
+        self.keep = keep
+        self._free = {}
+        self._lock = threading.Lock()
+
+    def __call__(self, shape, dtype) -> np.ndarray:
+        import weakref
+
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+        with self._lock:
+            blocks = self._free.get(n)
+            buf = blocks.pop() if blocks else None
+        if buf is None:
+            buf = np.empty(max(n, 1), np.uint8)
+        # every view NumPy derives from the result points at this holder (the buffer's exporter),
+        # so it outlives all of them and its finaliser is the release point
+        holder = (ctypes.c_char * max(n, 1)).from_buffer(buf)
+        weakref.finalize(holder, self._release, buf, n)
+        return np.frombuffer(holder, dtype=dtype, count=n // dtype.itemsize).reshape(shape)
+
+    def _release(self, buf, n) -> None:
+        with self._lock:
+            if len(self._free.get(n, ())) < self.keep:
+                self._free.setdefault(n, []).append(buf)
+
+    def clear(self) -> None:
+        with self._lock:
+            self._free.clear()
+            self.keep = 0
 
 
 def weight_names(n_layers: int) -> List[str]:

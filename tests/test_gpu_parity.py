@@ -174,16 +174,30 @@ def test_stories15m_greedy_dream_exact(tmpdir_mod, preset):
                                   g["dream_ids"])
 
 
-def test_streaming_load_matches(tmpdir_mod):
-    """keep_host_weights=False (read -> upload -> drop per tensor) gives identical logits."""
+def test_streaming_load_matches(tmpdir_mod, monkeypatch):
+    """keep_host_weights=False (read into page-locked buffers -> upload -> drop per tensor) and
+    the default (threaded reader, host copies kept) give the logits and host arrays the
+    reference's NpzFile loader gives (L3_NPZ_READER=npzfile)."""
     args = synth.tiny(2)
     _, path = _model(tmpdir_mod, args, synth.TINY_HIDDEN, 7, "sharp")
     ids = np.random.default_rng(2).integers(0, args.vocab_size, (2, 9))
-    a = llama3.Llama(path, args)(ids, 0)
+    monkeypatch.setattr(llama3, "_NPZ_READER", "npzfile")
+    ref_model = llama3.Llama(path, args)
+    a = ref_model(ids, 0)
+    monkeypatch.setattr(llama3, "_NPZ_READER", "threads")
+    k = llama3.Llama(path, args)
+    np.testing.assert_array_equal(k(ids, 0), a)
+    npz = np.load(path)
+    np.testing.assert_array_equal(k.tok_embedding, npz["model.embed_tokens.weight"])
+    np.testing.assert_array_equal(k.lm_head_weight, npz["lm_head.weight"].T)
+    np.testing.assert_array_equal(k.layers[1].feed_forward.down_weight,
+                                  npz["model.layers.1.mlp.down_proj.weight"].T)
     m = llama3.Llama(path, args, keep_host_weights=False)
     np.testing.assert_array_equal(m(ids, 0), a)
     with pytest.raises(RuntimeError, match="host copy not kept"):
         np.asarray(m.tok_embedding)
+    monkeypatch.setattr(llama3, "_NPZ_READER", "pinned")
+    np.testing.assert_array_equal(llama3.Llama(path, args, keep_host_weights=False)(ids, 0), a)
 
 
 def test_stories15m_live_oracle_gqa_batch(tmpdir_mod):

@@ -81,3 +81,21 @@ def test_streaming_npz_threaded_pieces(tmp_path):
     np.testing.assert_array_equal(s.get("a"), a)
     np.testing.assert_array_equal(s["b"], a[:7])
     s.close()
+
+
+def test_recycling_alloc_reuses_dropped_blocks():
+    """A member's buffer returns to the free list once the array and its views are gone."""
+    pool = utils.RecyclingAlloc(keep=2)
+    a = pool((4, 8), np.float32)
+    a[:] = 1
+    t = a.T  # a view keeps the block alive
+    addr = a.__array_interface__["data"][0]
+    del a
+    b = pool((4, 8), np.float32)
+    assert b.__array_interface__["data"][0] != addr
+    del t
+    c = pool((8, 4), np.float32)  # same byte size: the freed block comes back
+    assert c.__array_interface__["data"][0] == addr
+    pool.clear()
+    del b, c
+    assert not pool._free

@@ -1,8 +1,8 @@
-"""Streaming-loader probe: time ``Llama(path, args,
-keep_host_weights=False)`` on a Llama-3-shape ``.npz`` slice (D 4096, FD 14336, VS 128256,
-``--layers`` layers; 4 layers = 7.5 GB) with members read straight into page-locked buffers
-(``utils.StreamingNpz``, the default) against the NpzFile path (``L3_NPZ_PINNED=0``) and
-against ``keep_host_weights=True`` (every member held on the host, NpzFile reads).  Arms
+"""Loader probe: time ``Llama(path, args, keep_host_weights=...)`` on a
+Llama-3-shape ``.npz`` slice (D 4096, FD 14336, VS 128256, ``--layers`` layers; 4 layers =
+7.7 GB) for each reader (``L3_NPZ_READER``: ``utils.StreamingNpz`` into ordinary arrays — the
+default — or into recycled page-locked buffers, or NumPy's NpzFile), streaming
+(``keep_host_weights=False``) and with host copies kept.  Arms
 alternate in one process after a warm-up read, so the file is in the page cache for all of
 them (the probe measures the copy path, not the disk).  Prints one JSON line.
 
@@ -61,12 +61,16 @@ def main():
         gc.collect()
         ids = np.arange(8, dtype=np.int64).reshape(1, 8)
         ref = None
-        times = {"pinned_stream": [], "npzfile_stream": [], "keep_host": []}
+        # arm -> (reader, keep_host_weights)
+        arms = {"stream_threads": ("threads", False), "stream_pinned": ("pinned", False),
+                "stream_npzfile": ("npzfile", False), "keep_threads": ("threads", True),
+                "keep_npzfile": ("npzfile", True)}
+        times = {arm: [] for arm in arms}
         for rep in range(a.reps + 1):
-            for arm in times:
-                llama3._NPZ_PINNED = arm != "npzfile_stream"
+            for arm, (reader, keep) in arms.items():
+                llama3._NPZ_READER = reader
                 t0 = time.perf_counter()
-                m = llama3.Llama(path, args, device=0, keep_host_weights=arm == "keep_host")
+                m = llama3.Llama(path, args, device=0, keep_host_weights=keep)
                 dt = time.perf_counter() - t0
                 out = m(ids, 0)
                 if ref is None:
@@ -77,7 +81,7 @@ def main():
                 gc.collect()
                 if rep:  # rep 0 warms the page cache and the allocator
                     times[arm].append(dt)
-        llama3._NPZ_PINNED = True
+        llama3._NPZ_READER = "threads"
     res = {"probe": "streaming .npz load, Llama-3-shape slice", "layers": a.layers, "GB": round(gb, 2),
            "write_s": round(write_s, 2)}
     for arm, v in times.items():
