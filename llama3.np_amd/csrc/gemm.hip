@@ -133,8 +133,10 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
     // Rows per block: up to M = 8, a layer weight (<= 16 MB, L2-resident) runs one row per
     // block and re-reads W through L2 (B = 8 decode: QKV 13.7 -> 6.1 us, gate|up 12.3 -> 5.5
     // against 8-row blocks); the lm_head streams once with all rows per block (25 vs 37 us);
-    // past M = 8, 8-row blocks (B = 256: 0.75 vs 0.88 ms per step).  L3_GEMV_MR caps it (tuning).
-    static const int cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 8; }();
+    // past M = 8, 4-row blocks: twice the blocks of 8-row ones hide more of each block's round
+    // trips (batched decode B = 64 0.355 -> 0.316, B = 256 0.548 -> 0.530 ms per step; 2-row
+    // blocks 0.310 / 0.591).  L3_GEMV_MR caps it (tuning).
+    static const int cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 4; }();
     const bool small_w = (int64_t)a.N * a.K <= (int64_t)4 << 20;
     if (a.M <= 1 || cap == 1 || (small_w && a.M <= 8)) return launch_gemv_mr<EPI, 1>(a, s);
     if (a.M <= 2 || cap == 2) return launch_gemv_mr<EPI, 2>(a, s);
@@ -143,7 +145,7 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
 }
 
 bool gemv_direct(const GemmArgs& a) {
-    static const int cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 8; }();
+    static const int cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 4; }();
     const bool small_w = (int64_t)a.N * a.K <= (int64_t)4 << 20;
     return gemm_is_gemv(a) && (a.M <= 1 || cap == 1 || (small_w && a.M <= 8));
 }

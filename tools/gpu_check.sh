@@ -60,7 +60,10 @@ for s in "$@"; do
     declayer0) L3_DECODE_LAYER=0 step declayer0 300 python tools/bench_decode.py ;;
     decnofuse) L3_DECODE_FUSE_O=0 step decnofuse 300 python tools/bench_decode.py ;;
     testsdec) step testsdec 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "greedy or generate or decode or head_dims or cli or cache_edges or tiny or golden or speculative or run_ahead" --timeout 300 --timeout-method thread ;;
+    decmr2) L3_GEMV_MR=2 step decmr2 300 python tools/bench_decode.py ;;
+    decmr4) L3_GEMV_MR=4 step decmr4 300 python tools/bench_decode.py ;;
     decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
+    decprofb*) step $s 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$s -o run --output-format csv -- python tools/bench_decode.py --eager-batch ${s#decprofb} ;;
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
     c4) step c4 300 python bench.py --global-batch 2048 --steps 5 --warmup 1 --no-cpu-baseline --no-kernel-breakdown ;;
