@@ -150,6 +150,22 @@ bool gemv_direct(const GemmArgs& a) {
     return gemm_is_gemv(a) && (a.M <= 1 || cap == 1 || (small_w && a.M <= 8));
 }
 
+// 9..256 rows against a small weight on the skinny MFMA kernel (gemm_kernel.h); L3_SKINNY=0
+// keeps them on the GEMV (A/B)
+template <int EPI, int TN>
+static hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
+    constexpr int WN = 16 * TN;
+    const int64_t blocks = (int64_t)((a.M + 15) / 16) * ((a.N + WN - 1) / WN);
+    hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 6>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+static bool use_skinny(const GemmArgs& a) {
+    static const int on = [] { const char* e = getenv("L3_SKINNY"); return e ? atoi(e) : 1; }();
+    static const int lo = [] { const char* e = getenv("L3_SKINNY_MIN"); return e ? atoi(e) : 9; }();
+    return on && a.M >= lo && a.M <= 256 && !a.kv_bak && !a.parts && !a.amax_part && a.K % 16 == 0;
+}
+
 bool gemm_is_gemv(const GemmArgs& a) {
     const int mr = a.M <= 1 ? 1 : a.M <= 2 ? 2 : a.M <= 4 ? 4 : 8;
     const bool short_m = a.M <= 8 || (a.M <= 256 && (int64_t)a.N * a.K <= (int64_t)4 << 20);
@@ -180,6 +196,15 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         }
     }
     if (a.amax_part && (epi != EPI_STORE || !gemv_store_blocks(a))) return hipErrorInvalidValue;
+    if (gemm_is_gemv(a) && use_skinny(a)) {
+        switch (epi) {
+            case EPI_SWIGLU: return launch_skinny<EPI_SWIGLU, 2>(a, s);
+            case EPI_QKV: return launch_skinny<EPI_QKV, 1>(a, s);
+            case EPI_RESID: return launch_skinny<EPI_RESID, 1>(a, s);
+            case EPI_STORE: return launch_skinny<EPI_STORE, 1>(a, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     if (gemm_is_gemv(a)) {
         switch (epi) {
             case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);

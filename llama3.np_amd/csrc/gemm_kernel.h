@@ -550,6 +550,81 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
 #undef L3_STAMP
 
 // ---------------------------------------------------------------------------------------
+// Skinny MFMA GEMM for 9..256 rows against a small (L2-resident) weight: batched decode and
+// short prompts (llama3.py:166-178,211,99-102 at B x 1 tokens).  A block owns one 16-row x
+// 16*TN-column output tile and its four waves split K; no LDS staging: every lane loads its own
+// fragments straight from global memory (A row m0 + (l&15) and W rows n0 + 16j + (l&15),
+// 16-byte pieces at k = 16kb + 4(l>>4): the K-permutation of gemm_lds_kernel), up to CH
+// k-blocks of them in flight per memory round trip, then 4 MFMAs per k-block and W row.  The
+// four partial tiles (and row sums of squares) meet in LDS and wave 0 adds them in wave order
+// and runs the tiled kernel's epilogue (RMSNorm row factor, RoPE / KV append, SwiGLU pairs,
+// residual).  The weight-streaming GEMV keeps M <= 8, where its lanes' wider K split wins.
+template <int EPI, int TN, int CH>
+__global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs p) {
+    static_assert(EPI != EPI_SWIGLU || TN % 2 == 0, "SwiGLU pairs gate / up tiles");
+    constexpr int WN = 16 * TN;  // columns per tile
+    __shared__ f32x4 red[4][TN][64];
+    __shared__ float rss[4][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int frow = lane & 15, kq = 4 * (lane >> 4);
+    const int ntn = (p.N + WN - 1) / WN;
+    const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
+    const int m0 = mt * 16, n0 = nt * WN;
+    const float* arow = a_row(p, min(m0 + frow, p.M - 1));
+    const float* wrow[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) wrow[j] = p.W + (int64_t)min(n0 + 16 * j + frow, p.N - 1) * p.K;
+    f32x4 acc[1][TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss = 0.f;
+    const int nkb = p.K >> 4;
+    const int kb_lo = wid * nkb / 4, kb_hi = (wid + 1) * nkb / 4;  // this wave's k-blocks
+    for (int kb0 = kb_lo; kb0 < kb_hi; kb0 += CH) {
+        f32x4 av[CH], wv[CH][TN];
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const int k = 16 * min(kb0 + c, kb_hi - 1) + kq;
+            av[c] = *reinterpret_cast<const f32x4*>(arow + k);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) wv[c][j] = *reinterpret_cast<const f32x4*>(wrow[j] + k);
+        }
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            if (kb0 + c < kb_hi) {  // wave-uniform
+                ss += av[c].x * av[c].x + av[c].y * av[c].y + av[c].z * av[c].z + av[c].w * av[c].w;
+#pragma unroll
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[0][j] = mfma4(wv[c][j][s], av[c][s], acc[0][j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) red[wid][j][lane] = acc[0][j];
+    rss[wid][lane] = ss;
+    __syncthreads();
+    if (wid != 0) return;
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[0][j] += red[w][j][lane];
+        ss += rss[w][lane];
+    }
+    float rs[1];
+    {
+        const float v = sum_xor16_32(ss);  // the four k-quarters of the row
+        rs[0] = p.norm ? __builtin_amdgcn_rsqf(v * (1.0f / (float)p.K) + p.eps) : 1.0f;
+    }
+    if constexpr (EPI == EPI_QKV) {
+        qkv_epilogue<1, TN>(p, acc, rs, m0, n0, lane);
+    } else {
+        const f32x4 res[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+        direct_epilogue<1, TN, EPI, false, 1>(p, acc, rs, res, m0, n0, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Skinny GEMM for short M (greedy decode, short prompts): weight-streaming, HBM / latency
 // bound, so no MFMA; MR rows per block, grid.y row blocks beyond MR.  A unit is one W row (EPI_STORE / EPI_RESID), a RoPE pair (EPI_QKV: rows
 // 2u, 2u + 1) or a gate/up pair (EPI_SWIGLU: fused rows 32(u/16) + u%16 and + 16).  LPU lanes

@@ -780,6 +780,16 @@ def test_one_row_gemv_integer_exact(ctx, K, N):
     np.testing.assert_array_equal(ctx.op_linear(x, w), x @ w.T)
 
 
+@pytest.mark.parametrize("M", [9, 17, 64, 100, 256])
+def test_skinny_gemm_integer_exact(ctx, M):
+    """9..256 rows against a small weight (batched decode, short prompts) run the skinny MFMA
+    kernel (no LDS; K in the tiled kernel's order): integer operands, bit-exact."""
+    rng = np.random.default_rng(M)
+    x = rng.integers(-4, 5, (M, 288)).astype(np.float32)
+    w = rng.integers(-4, 5, (864, 288)).astype(np.float32)
+    np.testing.assert_array_equal(ctx.op_linear(x, w), x @ w.T)
+
+
 def test_generate_all_bounds_at_max_seq_len(tmpdir_mod):
     """The device loop's last decode step runs at position max_new_tokens - 1: max_new_tokens
     == max_seq_len is the longest legal run (ids equal the oracle's, the last step writing the

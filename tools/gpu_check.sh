@@ -60,6 +60,8 @@ for s in "$@"; do
     declayer0) L3_DECODE_LAYER=0 step declayer0 300 python tools/bench_decode.py ;;
     decnofuse) L3_DECODE_FUSE_O=0 step decnofuse 300 python tools/bench_decode.py ;;
     testsdec) step testsdec 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "greedy or generate or decode or head_dims or cli or cache_edges or tiny or golden or speculative or run_ahead" --timeout 300 --timeout-method thread ;;
+    decsk0) L3_SKINNY=0 step decsk0 300 python tools/bench_decode.py ;;
+    decskmin2) L3_SKINNY_MIN=2 step decskmin2 300 python tools/bench_decode.py ;;
     decmr2) L3_GEMV_MR=2 step decmr2 300 python tools/bench_decode.py ;;
     decmr4) L3_GEMV_MR=4 step decmr4 300 python tools/bench_decode.py ;;
     decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
