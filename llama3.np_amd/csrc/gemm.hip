@@ -135,9 +135,11 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
     // against 8-row blocks); the lm_head streams once with all rows per block (25 vs 37 us);
     // past M = 8, 4-row blocks: twice the blocks of 8-row ones hide more of each block's round
     // trips (batched decode B = 64 0.355 -> 0.316, B = 256 0.548 -> 0.530 ms per step; 2-row
-    // blocks 0.310 / 0.591).  L3_GEMV_MR caps it (tuning).
-    static const int cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 4; }();
+    // blocks 0.310 / 0.591; where the skinny MFMA kernel does not take them); a weight past the
+    // caches keeps one block row up to M = 8 so it streams once.  L3_GEMV_MR caps it (tuning).
+    static const int env_cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 0; }();
     const bool small_w = (int64_t)a.N * a.K <= (int64_t)4 << 20;
+    const int cap = env_cap ? env_cap : small_w ? 4 : 8;
     if (a.M <= 1 || cap == 1 || (small_w && a.M <= 8)) return launch_gemv_mr<EPI, 1>(a, s);
     if (a.M <= 2 || cap == 2) return launch_gemv_mr<EPI, 2>(a, s);
     if (a.M <= 4 || cap == 4) return launch_gemv_mr<EPI, 4>(a, s);
