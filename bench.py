@@ -9,12 +9,15 @@ norm + lm_head on the last position) of B=256 sequences x L=256 tokens per GPU,
 start_pos 0, ids already resident in HBM, logits left in HBM; for N > 1 each rank
 owns its 256 batch rows (weak scaling, reference rows are independent:
 llama3.py:163-211) and the step ends with the single RCCL gather of every rank's
-logits to rank 0 over xGMI (on the library's comm stream: step k's gather overlaps
-step k+1's layers; the timed region's closing synchronize waits for the last one).
+logits to rank 0 over xGMI (on the context stream, after the forward that wrote the rows).
 Rank 0 prints one JSON line.
 
 value: the product forward (layers as two batch-row ranges on two HIP streams,
-l3_set_batch_split), no events in the timed region.
+l3_set_batch_split; the last block's attention / O-proj / FFN on each sequence's last
+position, the only rows that reach the logits, l3_set_last_layer_rows — its QKV GEMM still
+appends every position to the KV cache), no events in the timed region; beside it
+ms_per_step_all_rows_last_layer, the same steps with every position through the last block.
+The roofline, per-kernel and C5 passes run every position of every layer.
 roofline: the dominant kernel is the fused gate|up GEMM (N = 2*FD = 1536, K = 288,
 M = 65,536 rows) — algorithmic FLOPs 2*M*K*N per launch over its mean HIP-event
 duration on the context stream, against the 157.3 TFLOP/s dense fp32 MFMA peak, timed in
@@ -247,6 +250,7 @@ def bench_c5(a):
     dims = l3hip.Dims(dim=D, n_layers=args.n_layers, n_heads=H, n_kv_heads=KVH, vocab_size=VS,
                       hidden_dim=FD, max_seq_len=L, max_batch_size=B, norm_eps=args.norm_eps)
     ctx = l3hip.Context(dims, 0)
+    ctx.set_last_layer_rows(True)  # the whole-forward TF/s counts every row of every layer
     rng = np.random.default_rng(0)
     pool = (rng.random(1 << 28, dtype=np.float32) * 2 - 1) * np.float32(0.02 * 3 ** 0.5)
 
@@ -480,6 +484,13 @@ def main():
     checked = check_gathered(ctx, dist, bpg, VS, gathered_dev) if step_gather else None
     dist.barrier()
 
+    # beside `value`: the same K steps with the last block run on every position (the product
+    # runs its attention / O-proj / FFN on each sequence's last position only: the rows that
+    # reach the logits; l3_set_last_layer_rows) — and every pass below counts full layers
+    ctx.set_last_layer_rows(True)
+    step()
+    elapsed_all_rows = timed_steps(a.steps)
+
     # roofline: the same K steps serialized (one row range, one stream) with HIP events around
     # the FFN GEMM launches only (12 per step) — with concurrent row ranges two kernels share
     # the CUs and a launch's duration no longer measures that kernel
@@ -490,6 +501,7 @@ def main():
     stats = ctx.kernel_stats()
     ctx.kernel_timing(False)
     ctx.set_batch_split(a.split if a.split is not None else 2)
+    ctx.set_last_layer_rows(False)
 
     # N > 1: the logits gather alone (untimed for `value`): its share of a step at this N,
     # which the overlapped gather hides behind the next step's layers
@@ -545,6 +557,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
         "ms_per_step_serialized": round(elapsed_serial / a.steps * 1e3, 4),
+        "ms_per_step_all_rows_last_layer": round(elapsed_all_rows / a.steps * 1e3, 4),
         "batch_split": a.split if a.split is not None else 2,
         "ms_per_step_with_logits_d2h": round(host_ms, 4),
         "host_path_tokens_per_s": round(T * dist.world * d2h_steps / elapsed_d2h, 1),
@@ -573,6 +586,7 @@ def main():
     if dist.world == 1 and not a.no_kernel_breakdown:
         # per-kernel breakdown from a separate (untimed, serialized) pass with all events on
         ctx.set_batch_split(1)
+        ctx.set_last_layer_rows(True)  # every launch of a kind full size
         ctx.kernel_timing(True)
         for _ in range(3):
             step()

@@ -113,6 +113,13 @@ int l3_forward_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
  * kernels: no tails to fill) and one part for graph-captured decode steps.
  * parts in [1, 4], min_tokens >= 1 (default 8192). */
 int l3_set_batch_split(l3_ctx* ctx, int32_t parts, int64_t min_tokens);
+/* Last layer of a model forward (extension; default on, env L3_LAST_LAYER_ALL_ROWS=1 turns it
+ * off): only each sequence's last position reaches the logits (llama3.py:304), so the last
+ * block runs its QKV GEMM on every position (the KV cache gets every slot, as the reference's)
+ * and its attention, O-proj and FFN on the last position only.  Logits and caches are the
+ * full block's (the attention of that row runs on the decode kernel: fp32 rounding differs
+ * from the prefill kernel's by ~1e-7).  all_rows != 0: every position through the whole block. */
+int l3_set_last_layer_rows(l3_ctx* ctx, int32_t all_rows);
 /* Same with device-resident ids (int32 [B, L]) and logits ([B, VS]); async. */
 int l3_forward_dev(l3_ctx* ctx, const int32_t* ids_dev, int32_t B, int32_t L,
                    int32_t start_pos, float* logits_dev);

@@ -198,7 +198,7 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         }
     }
     if (a.amax_part && (epi != EPI_STORE || !gemv_store_blocks(a))) return hipErrorInvalidValue;
-    if (gemm_is_gemv(a) && use_skinny(a)) {
+    if (a.force_skinny || (gemm_is_gemv(a) && use_skinny(a))) {
         switch (epi) {
             case EPI_SWIGLU: return launch_skinny<EPI_SWIGLU, 2>(a, s);
             case EPI_QKV: return launch_skinny<EPI_QKV, 1>(a, s);

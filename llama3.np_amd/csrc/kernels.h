@@ -57,6 +57,9 @@ struct GemmArgs {
     // row sums of squares [splits][M] there, and splitk_finish_kernel applies the epilogue
     float* ws; int64_t ws_cap;
     int splits;                    // set by launch_gemm
+    // the skinny MFMA kernel whatever M and W (a pruned last layer: every row rounds the same
+    // way for any batch split, runtime.hip run_layer last_rows)
+    bool force_skinny;
 };
 constexpr int GEMV_MAXP = 8;
 constexpr int KV_BAK_SLOTS = 32;  // > the decode steps ever run ahead (runtime.hip SPEC_AHEAD)
@@ -182,6 +185,8 @@ __device__ __forceinline__ const float* res_at(const GemmArgs& p, int64_t row, i
 
 struct AttnArgs {
     const float* q;       // [B*L, H*HD], pre-scaled by log2(e)/sqrt(HD)
+    int64_t q_ld;         // decode (L = 1) only: row stride of q in floats (0: H*HD); the last
+                          // layer of a pruned prefill reads each sequence's last q row in place
     const float* cache_k; // [maxB, KVH, Smax, HD]
     const float* cache_v;
     float* out;           // [B*L, H*HD]

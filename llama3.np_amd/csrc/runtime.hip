@@ -93,6 +93,8 @@ struct l3_ctx {
     hipStream_t aux[MAX_PARTS - 1] = {};
     hipEvent_t fork_ev = nullptr, join_ev[MAX_PARTS - 1] = {};
     int split = 2;                   // parts (1 = off); l3_set_batch_split, L3_BATCH_SPLIT
+    bool prune_last = true;          // last layer: attention / O-proj / FFN on the last rows only
+                                     // (l3_set_last_layer_rows, L3_LAST_LAYER_ALL_ROWS)
     int64_t split_min_tokens = 8192; // a part must hold at least this many tokens
     l3_dims d{};
     int HD = 0, qdim = 0, kvdim = 0, qkvn = 0;
@@ -319,6 +321,7 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     l3_ctx* c = new l3_ctx();
     c->device = device;
     c->d = d;
+    if (const char* e = getenv("L3_LAST_LAYER_ALL_ROWS")) c->prune_last = atoi(e) == 0;
     if (const char* e = getenv("L3_BATCH_SPLIT")) {  // default for new contexts
         const int n = atoi(e);
         c->split = n < 1 ? 1 : n > l3_ctx::MAX_PARTS ? l3_ctx::MAX_PARTS : n;
@@ -574,8 +577,17 @@ static int check_call(l3_ctx* c, int B, int L, int start_pos) {
 // emb_ids: layer 0 of a model forward reads its input rows straight from the embedding table
 // (llama3.py:287 fused into the QKV GEMM's A gather and the O-proj's residual), so no embed
 // kernel runs and h is first written by that O-proj
+// last_rows (a model forward's last layer, L > 1): only the last position of each sequence
+// reaches the output (llama3.py:304 keeps h[:, -1] of the last block), so after the QKV GEMM —
+// which still appends every position's K / V to the cache — the attention runs for that one
+// query per sequence (the decode kernel, reading the q row in place) and the O-proj, gate|up
+// and down run on B rows instead of B*L: the logits and every cache slot are what the full
+// layer gives (the other rows of h are never read again: the next forward starts from the
+// embedding).  Those GEMMs always take the skinny MFMA kernel, whose rows round the same way
+// at any M, so a batch split still gives bit-identical logits
 static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* pos_dev = nullptr,
-                     const int32_t* emb_ids = nullptr, int b0 = 0, hipStream_t s = nullptr) {
+                     const int32_t* emb_ids = nullptr, int b0 = 0, hipStream_t s = nullptr,
+                     bool last_rows = false) {
     // rows [b0, b0 + B) of the batch on stream s: every buffer is offset to batch row b0
     if (!s) s = c->stream;
     Layer& Ly = c->layers[li];
@@ -605,6 +617,28 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     float* skws = s == c->stream ? c->skws : nullptr;
     g.ws = skws; g.ws_cap = c->skws_cap;
     if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
+    if (last_rows && L > 1 && !emb_ids && !pos_dev) {
+        const int D4 = D;
+        float* hl = h + (int64_t)(L - 1) * D4;  // row b's last position: hl + b * L * D
+        AttnArgs a{};
+        a.q = q + (int64_t)(L - 1) * c->qdim; a.q_ld = (int64_t)L * c->qdim;
+        a.cache_k = Ly.cache_k + cache0; a.cache_v = Ly.cache_v + cache0; a.out = attn;  // [B, qdim]
+        a.B = B; a.L = 1; a.start_pos = start_pos + L - 1; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
+        a.HD = c->HD; a.Smax = c->d.max_seq_len;
+        if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention(a, s); })) return 1;
+        GemmArgs o{};  // O-proj + residual on the last rows, in place on h
+        o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.C = hl; o.ldc = (int64_t)L * D4;
+        o.M = B; o.N = D4; o.K = c->qdim; o.norm = false; o.force_skinny = true;
+        if (timed_on(c, L3_K_OPROJ, s, [&] { return launch_gemm(EPI_RESID, o, s); })) return 1;
+        GemmArgs gl{};  // rmsnorm -> gate|up -> SwiGLU on the last rows
+        gl.A = hl; gl.lda = (int64_t)L * D4; gl.W = Ly.wgu; gl.C = hid; gl.ldc = FD;
+        gl.M = B; gl.N = 2 * FD; gl.K = D4; gl.norm = true; gl.eps = c->d.norm_eps; gl.force_skinny = true;
+        if (timed_on(c, L3_K_GATEUP, s, [&] { return launch_gemm(EPI_SWIGLU, gl, s); })) return 1;
+        GemmArgs dl{};  // down + residual on the last rows
+        dl.A = hid; dl.lda = FD; dl.W = Ly.wd; dl.C = hl; dl.ldc = (int64_t)L * D4;
+        dl.M = B; dl.N = D4; dl.K = FD; dl.norm = false; dl.force_skinny = true;
+        return timed_on(c, L3_K_DOWN, s, [&] { return launch_gemm(EPI_RESID, dl, s); });
+    }
     GemmArgs gu{};  // rmsnorm -> gate|up -> SwiGLU
     gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
     gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true;  // n_ffn folded into wgu
@@ -717,10 +751,12 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
     for (int p = 0; p < parts && lm_parts; ++p)
         lm_parts = gemm_store_config(lm_head_args(c, nb[p], L, logits_dev, b0[p])) == lm_cfg;
     int rc = 0;
-    for (int li = 0; li < (int)c->layers.size() && !rc; ++li) {
+    const int nl = (int)c->layers.size();
+    for (int li = 0; li < nl && !rc; ++li) {
         roctxRangePushA(names[li < 8 ? li : 8]);
         for (int p = 0; p < parts && !rc; ++p)
-            rc = run_layer(c, li, nb[p], L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr, b0[p], st[p]);
+            rc = run_layer(c, li, nb[p], L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr, b0[p], st[p],
+                           c->prune_last && li == nl - 1 && li > 0);
         roctxRangePop();
     }
     // the previous step's gather may still read the logits rows: the lm_head streams wait for
@@ -800,6 +836,12 @@ extern "C" int l3_set_batch_split(l3_ctx* c, int32_t parts, int64_t min_tokens) 
     if (min_tokens < 1) return fail("l3_set_batch_split: min_tokens %lld < 1", (long long)min_tokens);
     c->split = parts;
     c->split_min_tokens = min_tokens;
+    return 0;
+}
+
+extern "C" int l3_set_last_layer_rows(l3_ctx* c, int32_t all_rows) {
+    CHECK_CTX(c);
+    c->prune_last = all_rows == 0;
     return 0;
 }
 

@@ -75,6 +75,7 @@ _SIGNATURES = {
     "l3_d2h": (ctypes.c_int, [_P, _P, _P, _SZ]),
     "l3_synchronize": (ctypes.c_int, [_P]),
     "l3_set_batch_split": (ctypes.c_int, [_P, _I32, _I64]),
+    "l3_set_last_layer_rows": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_timing": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
     "l3_decode_stats": (ctypes.c_int, [_P, _P, _P]),
@@ -293,6 +294,11 @@ class Context:
         """Run a model forward as `parts` batch-row ranges on their own streams (extension;
         results bit-identical for any split, default 2)."""
         check(lib().l3_set_batch_split(self._h, int(parts), int(min_tokens)))
+
+    def set_last_layer_rows(self, all_rows: bool) -> None:
+        """Extension: False (default) runs the last block's attention / O-proj / FFN on each
+        sequence's last position only (l3_set_last_layer_rows); True, every position."""
+        check(lib().l3_set_last_layer_rows(self._h, int(bool(all_rows))))
 
     def synchronize(self) -> None:
         check(lib().l3_synchronize(self._h))

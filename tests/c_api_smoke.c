@@ -117,6 +117,15 @@ int main(void) {
         fprintf(stderr, "FAIL batch split changed the logits\n");
         return 1;
     }
+    // last block on every position (extension): the same logits within fp32 rounding
+    CHECK(l3_set_last_layer_rows(c, 1));
+    CHECK(l3_forward_host(c, ids, B, L, 0, logits2));
+    for (int i = 0; i < B * VS; ++i)
+        if (fabsf(logits[i] - logits2[i]) > 1e-4f) {
+            fprintf(stderr, "FAIL all-rows last layer differs at %d: %g vs %g\n", i, logits[i], logits2[i]);
+            return 1;
+        }
+    CHECK(l3_set_last_layer_rows(c, 0));
     free(logits2);
     CHECK(l3_set_batch_split(c, 1, 1));
     int64_t nxt[B];

@@ -790,6 +790,26 @@ def test_skinny_gemm_integer_exact(ctx, M):
     np.testing.assert_array_equal(ctx.op_linear(x, w), x @ w.T)
 
 
+def test_last_layer_last_rows_equals_all_rows(tmpdir_mod):
+    """The product forward runs the last block's attention / O-proj / FFN on each sequence's
+    last position only (l3_set_last_layer_rows; llama3.py:304 keeps h[:, -1]): logits equal the
+    all-rows forward's within fp32 rounding, and the KV caches it leaves (QKV still appends every
+    position) give the same next decode step — logits and greedy ids."""
+    args = synth.stories15m(8)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    ids = np.random.default_rng(77).integers(0, args.vocab_size, (8, 100))
+    pruned = llama3.Llama(path, args)
+    full = llama3.Llama(path, args)
+    full.context.set_last_layer_rows(True)
+    a, b = pruned(ids, 0), full(ids, 0)
+    assert float(np.max(np.abs(a - b))) <= 1e-5
+    nxt = np.argmax(b[:, 0, :], axis=-1).reshape(-1, 1)
+    ia, la = pruned.context.greedy_step(nxt, 100, want_logits=True)
+    ib, lb = full.context.greedy_step(nxt, 100, want_logits=True)
+    np.testing.assert_array_equal(ia, ib)
+    assert float(np.max(np.abs(la - lb))) <= 1e-5
+
+
 def test_generate_all_bounds_at_max_seq_len(tmpdir_mod):
     """The device loop's last decode step runs at position max_new_tokens - 1: max_new_tokens
     == max_seq_len is the longest legal run (ids equal the oracle's, the last step writing the
