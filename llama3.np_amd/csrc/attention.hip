@@ -56,6 +56,36 @@ static hipError_t launch_decode(const AttnArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// The last query rows of each sequence only (a pruned last block, runtime.hip run_layer): one
+// workgroup per (batch, head group) with one q-block per wave over rows [L - QW, L) — the
+// same kernel and per-query arithmetic as the full launch, so those rows are bit-identical
+template <int HD, int KT>
+static hipError_t launch_last_hd(AttnArgs a, hipStream_t s) {
+    const int n_rep = a.H / a.KVH;
+    const int G = n_rep % 4 == 0 ? 4 : n_rep % 2 == 0 ? 2 : 1;
+    const int QW = 16 * (4 / G);
+    a.q_first = a.L > QW ? a.L - QW : 0;
+    dim3 grid(1, a.H / G, a.B), block(256);
+    if (G == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 4, KT>), grid, block, 0, s, a);
+    else if (G == 2) hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, KT>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 1, KT>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_attention_last(const AttnArgs& a, hipStream_t s) {
+    if (a.B <= 0 || a.L <= 0) return hipSuccess;
+    if (a.KVH <= 0 || a.H % a.KVH != 0 || a.wo || a.pos_dev) return hipErrorInvalidValue;
+    switch (a.HD) {
+        case 16: return launch_last_hd<16, 64>(a, s);
+        case 32: return launch_last_hd<32, 64>(a, s);
+        case 48: return launch_last_hd<48, 64>(a, s);
+        case 64: return launch_last_hd<64, 64>(a, s);
+        case 96: return launch_last_hd<96, 32>(a, s);
+        case 128: return launch_last_hd<128, 32>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s) {
     if (a.B <= 0 || a.L <= 0) return hipSuccess;
     if (a.KVH <= 0 || a.H % a.KVH != 0) return hipErrorInvalidValue;

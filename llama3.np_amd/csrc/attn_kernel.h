@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
         qblk[j] = (j & 1) ? (2 * WPH * (j >> 1) + 2 * WPH - 1 - part) : (2 * WPH * (j >> 1) + part);
 
     const int start_pos = start_of(p);
-    const int q_lo = qt * QW;
+    const int q_lo = p.q_first + qt * QW;
     const int q_hi = min(p.L, q_lo + QW);
     const int key_end = start_pos + q_hi;  // keys [0, key_end) are needed
     const int ntiles = (key_end + KT - 1) / KT;
@@ -348,7 +348,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
 #pragma unroll
         for (int i = 0; i < WQ; ++i) wpre[i] = ok ? w4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    const f32x4* q4 = reinterpret_cast<const f32x4*>(p.q + (int64_t)b * (p.q_ld ? p.q_ld : (int64_t)p.H * HD) + h * HD);
+    const f32x4* q4 = reinterpret_cast<const f32x4*>(p.q + ((int64_t)b * p.H + h) * HD);
     f32x4 q[D4];
 #pragma unroll
     for (int i = 0; i < D4; ++i) q[i] = q4[i];

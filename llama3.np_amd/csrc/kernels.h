@@ -185,8 +185,8 @@ __device__ __forceinline__ const float* res_at(const GemmArgs& p, int64_t row, i
 
 struct AttnArgs {
     const float* q;       // [B*L, H*HD], pre-scaled by log2(e)/sqrt(HD)
-    int64_t q_ld;         // decode (L = 1) only: row stride of q in floats (0: H*HD); the last
-                          // layer of a pruned prefill reads each sequence's last q row in place
+    int q_first;          // prefill: first query row of the launch (grid.x covers [q_first, L));
+                          // a pruned last block runs only the last query rows of each sequence
     const float* cache_k; // [maxB, KVH, Smax, HD]
     const float* cache_v;
     float* out;           // [B*L, H*HD]
@@ -208,6 +208,7 @@ __device__ __forceinline__ int start_of(const Args& p) {
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
+hipError_t launch_attention_last(const AttnArgs& a, hipStream_t s);
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
                          DecState* st = nullptr);
 // the same result from the lm_head's per-block partials (one row: GemmArgs::amax_part)

@@ -579,8 +579,9 @@ static int check_call(l3_ctx* c, int B, int L, int start_pos) {
 // kernel runs and h is first written by that O-proj
 // last_rows (a model forward's last layer, L > 1): only the last position of each sequence
 // reaches the output (llama3.py:304 keeps h[:, -1] of the last block), so after the QKV GEMM —
-// which still appends every position's K / V to the cache — the attention runs for that one
-// query per sequence (the decode kernel, reading the q row in place) and the O-proj, gate|up
+// which still appends every position's K / V to the cache — the attention runs for the last
+// q-blocks only (launch_attention_last: the same kernel, so the last row is bit-identical to the
+// full launch's) and the O-proj, gate|up
 // and down run on B rows instead of B*L: the logits and every cache slot are what the full
 // layer gives (the other rows of h are never read again: the next forward starts from the
 // embedding).  Those GEMMs always take the skinny MFMA kernel, whose rows round the same way
@@ -620,14 +621,14 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     if (last_rows && L > 1 && !emb_ids && !pos_dev) {
         const int D4 = D;
         float* hl = h + (int64_t)(L - 1) * D4;  // row b's last position: hl + b * L * D
-        AttnArgs a{};
-        a.q = q + (int64_t)(L - 1) * c->qdim; a.q_ld = (int64_t)L * c->qdim;
-        a.cache_k = Ly.cache_k + cache0; a.cache_v = Ly.cache_v + cache0; a.out = attn;  // [B, qdim]
-        a.B = B; a.L = 1; a.start_pos = start_pos + L - 1; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
+        AttnArgs a{};  // the last query rows of each sequence (bit-identical to the full launch)
+        a.q = q; a.cache_k = Ly.cache_k + cache0; a.cache_v = Ly.cache_v + cache0; a.out = attn;
+        a.B = B; a.L = L; a.start_pos = start_pos; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
         a.HD = c->HD; a.Smax = c->d.max_seq_len;
-        if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention(a, s); })) return 1;
+        if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention_last(a, s); })) return 1;
         GemmArgs o{};  // O-proj + residual on the last rows, in place on h
-        o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.C = hl; o.ldc = (int64_t)L * D4;
+        o.A = attn + (int64_t)(L - 1) * c->qdim; o.lda = (int64_t)L * c->qdim;
+        o.W = Ly.wo; o.C = hl; o.ldc = (int64_t)L * D4;
         o.M = B; o.N = D4; o.K = c->qdim; o.norm = false; o.force_skinny = true;
         if (timed_on(c, L3_K_OPROJ, s, [&] { return launch_gemm(EPI_RESID, o, s); })) return 1;
         GemmArgs gl{};  // rmsnorm -> gate|up -> SwiGLU on the last rows

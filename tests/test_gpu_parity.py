@@ -791,10 +791,11 @@ def test_skinny_gemm_integer_exact(ctx, M):
 
 
 def test_last_layer_last_rows_equals_all_rows(tmpdir_mod):
-    """The product forward runs the last block's attention / O-proj / FFN on each sequence's
-    last position only (l3_set_last_layer_rows; llama3.py:304 keeps h[:, -1]): logits equal the
-    all-rows forward's within fp32 rounding, and the KV caches it leaves (QKV still appends every
-    position) give the same next decode step — logits and greedy ids."""
+    """The product forward runs the last block's attention on the last q-blocks and its O-proj /
+    FFN on each sequence's last position only (l3_set_last_layer_rows; llama3.py:304 keeps
+    h[:, -1]): the logits are those of the all-rows forward (same attention kernel for that row;
+    the skinny GEMMs round like the tiled ones up to fp32 ulps), and the KV caches it leaves (QKV
+    still appends every position) give the same next decode step — logits and greedy ids."""
     args = synth.stories15m(8)
     _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
     ids = np.random.default_rng(77).integers(0, args.vocab_size, (8, 100))
