@@ -88,7 +88,7 @@ __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&ac
     int sec[TN], head[TN], d[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-        const int col = min(ncol0 + j * 16 + fq4, p.N - 4);
+        const int col = min(ncol0 + j * 16 + fq4, p.N - 4) + p.col_base;
         sec[j] = col < qdim ? 0 : (col < qdim + kvdim ? 1 : 2);
         const int cc = col - (sec[j] == 0 ? 0 : (sec[j] == 1 ? qdim : qdim + kvdim));
         head[j] = cc / p.HD;

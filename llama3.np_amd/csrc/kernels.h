@@ -33,6 +33,9 @@ struct GemmArgs {
     int L, start_pos, H, KVH, HD, Smax;
     const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
+    int col_base;                  // EPI_QKV on the tiled / skinny kernels: index of output column 0
+                                   // in the [q | k | v] layout (W starts at that row of wqkv): a
+                                   // pruned last block appends K / V for every row without q
     // EPI_QKV on the GEMV (captured batch-1..8 decode steps): before appending K / V at pos, keep
     // the slot's previous contents in kv_bak [pos % KV_BAK_SLOTS][2: k, v][M][KVH][HD], so decode
     // steps run ahead of the caller can be undone (runtime.hip, speculate / spec_resolve)

@@ -579,9 +579,9 @@ static int check_call(l3_ctx* c, int B, int L, int start_pos) {
 // kernel runs and h is first written by that O-proj
 // last_rows (a model forward's last layer, L > 1): only the last position of each sequence
 // reaches the output (llama3.py:304 keeps h[:, -1] of the last block), so after the QKV GEMM —
-// which still appends every position's K / V to the cache — the attention runs for the last
-// q-blocks only (launch_attention_last: the same kernel, so the last row is bit-identical to the
-// full launch's) and the O-proj, gate|up
+// which still appends every position's K / V to the cache, and past 256 rows computes q for the
+// last rows only (a second, B-row QKV GEMM; the attention then runs the decode kernel, one
+// query per sequence), else the last q-blocks of the prefill attention — and the O-proj, gate|up
 // and down run on B rows instead of B*L: the logits and every cache slot are what the full
 // layer gives (the other rows of h are never read again: the next forward starts from the
 // embedding).  Those GEMMs always take the skinny MFMA kernel, whose rows round the same way
@@ -617,17 +617,33 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     // past launch_split's range, so no two streams ever share it)
     float* skws = s == c->stream ? c->skws : nullptr;
     g.ws = skws; g.ws_cap = c->skws_cap;
+    const bool prune = last_rows && L > 1 && !emb_ids && !pos_dev;
+    // a pruned block with more than 256 rows (the tiled QKV kernel): K / V for every row, q for
+    // the last row of each sequence only (its RoPE at position start_pos + L - 1)
+    const bool kv_only = prune && T > 256;
+    if (kv_only) { g.W = Ly.wqkv + (int64_t)c->qdim * D; g.N = 2 * c->kvdim; g.col_base = c->qdim; }
     if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
-    if (last_rows && L > 1 && !emb_ids && !pos_dev) {
+    if (prune) {
         const int D4 = D;
         float* hl = h + (int64_t)(L - 1) * D4;  // row b's last position: hl + b * L * D
-        AttnArgs a{};  // the last query rows of each sequence (bit-identical to the full launch)
-        a.q = q; a.cache_k = Ly.cache_k + cache0; a.cache_v = Ly.cache_v + cache0; a.out = attn;
-        a.B = B; a.L = L; a.start_pos = start_pos; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads;
-        a.HD = c->HD; a.Smax = c->d.max_seq_len;
-        if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention_last(a, s); })) return 1;
+        AttnArgs a{};
+        a.cache_k = Ly.cache_k + cache0; a.cache_v = Ly.cache_v + cache0; a.out = attn;
+        a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads; a.HD = c->HD; a.Smax = c->d.max_seq_len;
         GemmArgs o{};  // O-proj + residual on the last rows, in place on h
-        o.A = attn + (int64_t)(L - 1) * c->qdim; o.lda = (int64_t)L * c->qdim;
+        if (kv_only) {
+            GemmArgs gq = g;  // q of the last rows: [B, qdim], compact
+            gq.A = hl; gq.lda = (int64_t)L * D4; gq.W = Ly.wqkv; gq.N = c->qdim; gq.col_base = 0;
+            gq.M = B; gq.L = 1; gq.start_pos = start_pos + L - 1; gq.force_skinny = true;
+            gq.ws = nullptr;
+            if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, gq, s); })) return 1;
+            a.q = q; a.B = B; a.L = 1; a.start_pos = start_pos + L - 1;  // one query per sequence
+            if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention(a, s); })) return 1;
+            o.A = attn; o.lda = c->qdim;
+        } else {  // the last q-blocks of the full launch (same per-query arithmetic)
+            a.q = q; a.B = B; a.L = L; a.start_pos = start_pos;
+            if (timed_on(c, L3_K_ATTN, s, [&] { return launch_attention_last(a, s); })) return 1;
+            o.A = attn + (int64_t)(L - 1) * c->qdim; o.lda = (int64_t)L * c->qdim;
+        }
         o.W = Ly.wo; o.C = hl; o.ldc = (int64_t)L * D4;
         o.M = B; o.N = D4; o.K = c->qdim; o.norm = false; o.force_skinny = true;
         if (timed_on(c, L3_K_OPROJ, s, [&] { return launch_gemm(EPI_RESID, o, s); })) return 1;
