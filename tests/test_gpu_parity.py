@@ -212,6 +212,12 @@ def test_stories15m_live_oracle_gqa_batch(tmpdir_mod):
     b = rng.integers(0, args.vocab_size, (3, 7))
     assert _close(m(a, 0), ref(a, 0)) <= 1e-4
     assert _close(m(b, 100), ref(b, 100)) <= 1e-4
+    # a second 100-token chunk at 107 (T = 300: the pruned last block's K / V-only QKV, q of the
+    # last rows at positions 206, attending every cached slot), then one decode step at 207
+    c = rng.integers(0, args.vocab_size, (3, 100))
+    assert _close(m(c, 107), ref(c, 107)) <= 1e-4
+    d = rng.integers(0, args.vocab_size, (3, 1))
+    assert _close(m(d, 207), ref(d, 207)) <= 1e-4
 
 
 def test_transformer_block_and_attention_standalone():
