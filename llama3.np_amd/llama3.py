@@ -262,7 +262,10 @@ class Llama:
 
     Weights are uploaded once to HBM; ``__call__`` keeps activations
     device-resident across all layers and copies back only the last-position
-    logits.  ``generate`` runs argmax on the device and copies back only ids."""
+    logits (the last block runs its attention / O-proj / FFN for that position only
+    — the only rows llama3.py:304 keeps — while its K / V cache append still covers
+    every position; ``context.set_last_layer_rows(True)`` runs every row).
+    ``generate`` runs argmax on the device and copies back only ids."""
 
     def __init__(self, model_path: str, args: ModelArgs, device: Optional[int] = None,
                  keep_host_weights: bool = True):
