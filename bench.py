@@ -1,7 +1,8 @@
 """Benchmark: stories15M batched prefill on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--global-batch G]
-    (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+    N > 1: either under python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N,
+    or plain `python bench.py --gpus N`, which starts the N rank processes itself (spawn_ranks)
     --global-batch G: strong scaling instead (G rows split over the N GPUs; C4 is G = 2048)
 
 One step = one full forward (Llama.__call__ semantics: embedding, 6 blocks, final
@@ -56,17 +57,81 @@ PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
 B_PER_GPU, SEQ = 256, 256
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, argv, cmd=None, timeout_s=None, grace_s=20.0, out=None):
+    """``--gpus N`` with no launcher (WORLD_SIZE unset): start N fresh rank processes, one per
+    GPU, the way torch.distributed.run would, and wait for them.
+
+    Called before this process makes any GPU call (the ranks are children started with
+    subprocess, never exec'd over this process).  Each child gets RANK / LOCAL_RANK /
+    WORLD_SIZE / LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT and an
+    L3_LAUNCH_KEY unique to this launch (the RCCL-id hand-off file, l3hip.launch_key()).
+    Rank 0's stdout is this process's stdout (its one JSON line is the bench line); the other
+    ranks' stdout goes to stderr.  If any rank fails, the ranks still running are given
+    ``grace_s`` and then killed by pid (a peer blocked in an RCCL call never returns on its
+    own), and the first failing rank's exit status is returned; 0 when every rank succeeded.
+    ``cmd`` (tests) replaces the rank body ``[python, bench.py] + argv``."""
+    import subprocess
+    import uuid
+
+    port = _free_port()
+    key = f"spawn_{os.getpid()}_{port}_{uuid.uuid4().hex[:12]}"
+    base = list(cmd) if cmd else [sys.executable, "-u", os.path.abspath(__file__)]
+    out = sys.stdout if out is None else out
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), L3_LAUNCH_KEY=key)
+        procs.append(subprocess.Popen(base + list(argv), env=env,
+                                      stdout=out if r == 0 else sys.stderr))
+    t0 = time.time()
+    first_bad, bad_at = None, None
+    while True:
+        rcs = [p.poll() for p in procs]
+        for r, rc in enumerate(rcs):
+            if rc not in (None, 0) and first_bad is None:
+                first_bad, bad_at = (r, rc), time.time()
+        if all(rc is not None for rc in rcs):
+            break
+        late = timeout_s is not None and time.time() - t0 > timeout_s
+        if late or (bad_at is not None and time.time() - bad_at > grace_s):
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()  # the exact child pid this function started
+            for p in procs:
+                p.wait()
+            if first_bad is None:
+                first_bad = (-1, 124)
+            break
+        time.sleep(0.05)
+    if first_bad is not None:
+        r, rc = first_bad
+        print(json.dumps({"error": "rank failed" if r >= 0 else "ranks timed out", "rank": r,
+                          "rc": rc, "world": n}), file=sys.stderr, flush=True)
+        return rc if isinstance(rc, int) and rc > 0 else 1
+    return 0
+
+
 class Dist:
-    """One process per GPU (torchrun env).  No PyTorch in this process: the RCCL id goes
-    rank 0 -> peers through an atomically renamed file (single node, l3hip.launch_key()), and
-    barriers / the max-over-ranks time run over RCCL itself."""
+    """One process per GPU (torch.distributed.run env, or the ranks spawn_ranks started).  No
+    PyTorch in this process: the RCCL id goes rank 0 -> peers through an atomically renamed
+    file (single node, l3hip.launch_key()), and barriers / the max-over-ranks time run over
+    RCCL itself."""
 
     def __init__(self, n, force_comm=False):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         if n != self.world:
-            raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}; launch N>1 with torch.distributed.run")
+            raise SystemExit(f"--gpus {n} but WORLD_SIZE={self.world}")
         self.ctx = None
         self.force_comm = force_comm
 
@@ -94,7 +159,14 @@ class Dist:
 
 def cpu_baseline():
     """Oracle (port of the reference's NumPy forward) on the C3 workload itself, SURVEY 8(d):
-    B=256, L=256, one warm-up forward, median of 3; plus a 1-thread figure on a B=4 sample."""
+    B=256, L=256, one warm-up forward, median of 3, OpenBLAS on every thread this process may
+    use; plus a 1-thread figure on a labelled sample of the same workload (16 of its 256 rows:
+    the rows are independent, llama3.py:163-211, so the rate per row is the C3 rate).
+
+    Thread count: OpenBLAS takes OPENBLAS_NUM_THREADS, else OMP_NUM_THREADS.  The GPU box
+    exports OMP_NUM_THREADS=16 — its CPU share per GPU, which its rules say to leave as set —
+    so on the box the figure is 16 threads of a 256-CPU host, and the line says so
+    (cores / nproc / affinity / thread_cap)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import llama3_oracle as orc
 
@@ -103,7 +175,16 @@ def cpu_baseline():
 
         blas = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
     except Exception:
-        blas = int(os.environ.get("OPENBLAS_NUM_THREADS", os.cpu_count() or 1))
+        blas = int(os.environ.get("OPENBLAS_NUM_THREADS", os.environ.get("OMP_NUM_THREADS", 1)))
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = None
+    cap = None
+    for var in ("OPENBLAS_NUM_THREADS", "OMP_NUM_THREADS"):
+        if os.environ.get(var):
+            cap = f"{var}={os.environ[var]}"
+            break
     Bs = B_PER_GPU
     args = synth.stories15m(Bs)
     w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=0)
@@ -116,24 +197,28 @@ def cpu_baseline():
         model(ids, 0)
         times.append(time.perf_counter() - t0)
     t = float(np.median(times))
-    one = None
+    one, B1 = None, 16
     try:
         from threadpoolctl import threadpool_limits
 
         with threadpool_limits(limits=1):
             t1 = time.perf_counter()
-            model(ids[:4], 0)
-            one = round(4 * SEQ / (time.perf_counter() - t1), 1)
+            model(ids[:B1], 0)
+            one = round(B1 * SEQ / (time.perf_counter() - t1), 1)
     except Exception:
         pass
     return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(blas),
-            "nproc": os.cpu_count(), "openblas_threads": int(blas),
-            "value_1_thread": one,
+            "nproc": os.cpu_count(), "affinity": affinity, "openblas_threads": int(blas),
+            "thread_cap": cap,
+            "value_1_thread_sample": one,
+            "sample_1_thread": f"B={B1} of the C3 batch's {Bs} rows, L={SEQ}, one forward, "
+                               f"OpenBLAS limited to 1 thread (rows independent: same per-row work)",
             "kind": "port",
             "sample": f"oracle/llama3_oracle.py (NumPy restatement of the reference, f64 after layer-0 "
                       f"RoPE as the reference) stories15M prefill B={Bs} L={SEQ} (the C3 workload), "
                       f"1 warm-up, median of 3 ({', '.join(f'{x:.2f}' for x in times)} s), "
-                      f"OpenBLAS threads={blas} of nproc={os.cpu_count()}; value_1_thread: B=4 sample"}
+                      f"OpenBLAS threads={blas} of nproc={os.cpu_count()} "
+                      f"(affinity {affinity}; cap: {cap or 'none'})"}
 
 
 def traffic_per_launch(rows):
@@ -147,37 +232,37 @@ def traffic_per_launch(rows):
     return d.get("hbm_bytes_per_launch")
 
 
+W_KINDS = {"self_attn.q_proj.weight": l3hip.W_Q, "self_attn.k_proj.weight": l3hip.W_K,
+           "self_attn.v_proj.weight": l3hip.W_V, "self_attn.o_proj.weight": l3hip.W_O,
+           "mlp.gate_proj.weight": l3hip.W_GATE, "mlp.up_proj.weight": l3hip.W_UP,
+           "mlp.down_proj.weight": l3hip.W_DOWN, "input_layernorm.weight": l3hip.W_ATTN_NORM,
+           "post_attention_layernorm.weight": l3hip.W_FFN_NORM}
+
+
+def upload_weights(ctx, w, n_layers):
+    """Every tensor of a weight mapping through the C ABI (what Llama.__init__ does from an .npz),
+    then finalize."""
+    ctx.upload(0, l3hip.W_EMBED, w["model.embed_tokens.weight"])
+    for i in range(n_layers):
+        for name, kind in W_KINDS.items():
+            ctx.upload(i, kind, w[f"model.layers.{i}.{name}"])
+    ctx.upload(0, l3hip.W_FINAL_NORM, w["model.norm.weight"])
+    ctx.upload(0, l3hip.W_LM_HEAD, w["lm_head.weight"])
+    ctx.finalize()
+
+
 def c5_context(n_layers, B, L):
     """A Llama-3-8B-shaped context (D 4096, H 32 / KVH 8, FD 14336, VS 128256) with synthetic
-    weights uploaded tensor by tensor through the C ABI (uniform, std 0.02, drawn from a
-    256M-float pool: an 8.5G-sample normal draw would take minutes)."""
+    weights uploaded tensor by tensor through the C ABI (synth.pool_weights: views of a uniform
+    256M-float pool, std 0.02 — an 8.5G-sample normal draw would take minutes)."""
     args = synth.llama3_shape(n_layers=n_layers, max_batch_size=B, max_seq_len=L)
-    D, FD, VS, H, KVH = args.dim, synth.LLAMA3_HIDDEN, args.vocab_size, args.n_heads, args.kv_heads
-    HD = D // H
-    dims = l3hip.Dims(dim=D, n_layers=args.n_layers, n_heads=H, n_kv_heads=KVH, vocab_size=VS,
-                      hidden_dim=FD, max_seq_len=L, max_batch_size=B, norm_eps=args.norm_eps)
+    dims = l3hip.Dims(dim=args.dim, n_layers=args.n_layers, n_heads=args.n_heads,
+                      n_kv_heads=args.kv_heads, vocab_size=args.vocab_size,
+                      hidden_dim=synth.LLAMA3_HIDDEN, max_seq_len=L, max_batch_size=B,
+                      norm_eps=args.norm_eps)
     ctx = l3hip.Context(dims, 0)
     rng = np.random.default_rng(0)
-    pool = (rng.random(1 << 28, dtype=np.float32) * 2 - 1) * np.float32(0.02 * 3 ** 0.5)
-
-    def tensor(shape):
-        n = int(np.prod(shape))
-        if n <= pool.size:
-            o = int(rng.integers(0, pool.size - n + 1))
-            return pool[o:o + n].reshape(shape)
-        return np.resize(pool, n).reshape(shape)
-
-    ctx.upload(0, l3hip.W_EMBED, np.resize(pool * np.float32(50.0), VS * D).reshape(VS, D))
-    for i in range(args.n_layers):
-        for kind, shape in ((l3hip.W_Q, (H * HD, D)), (l3hip.W_K, (KVH * HD, D)), (l3hip.W_V, (KVH * HD, D)),
-                            (l3hip.W_O, (D, H * HD)), (l3hip.W_GATE, (FD, D)), (l3hip.W_UP, (FD, D)),
-                            (l3hip.W_DOWN, (D, FD))):
-            ctx.upload(i, kind, tensor(shape))
-        ctx.upload(i, l3hip.W_ATTN_NORM, np.ones(D, np.float32))
-        ctx.upload(i, l3hip.W_FFN_NORM, np.ones(D, np.float32))
-    ctx.upload(0, l3hip.W_FINAL_NORM, np.ones(D, np.float32))
-    ctx.upload(0, l3hip.W_LM_HEAD, tensor((VS, D)))
-    ctx.finalize()
+    upload_weights(ctx, synth.pool_weights(args, synth.LLAMA3_HIDDEN, rng=rng), args.n_layers)
     return ctx, args, rng
 
 
@@ -243,36 +328,12 @@ def bench_c5(a):
     Weights (32 GB fp32) are synthetic and uploaded tensor by tensor through the C ABI
     (uniform with std 0.02 drawn from a 256M-float pool: an 8.5G-sample normal draw would take
     minutes); the forward is the same l3_forward_dev as the headline bench."""
-    args = synth.llama3_shape(n_layers=a.layers, max_batch_size=64, max_seq_len=2048)
+    B, L = 64, 2048
+    t_up = time.perf_counter()
+    ctx, args, rng = c5_context(a.layers, B, L)
     D, FD, VS, H, KVH = args.dim, synth.LLAMA3_HIDDEN, args.vocab_size, args.n_heads, args.kv_heads
     HD = D // H
-    B, L = 64, 2048
-    dims = l3hip.Dims(dim=D, n_layers=args.n_layers, n_heads=H, n_kv_heads=KVH, vocab_size=VS,
-                      hidden_dim=FD, max_seq_len=L, max_batch_size=B, norm_eps=args.norm_eps)
-    ctx = l3hip.Context(dims, 0)
     ctx.set_last_layer_rows(True)  # the whole-forward TF/s counts every row of every layer
-    rng = np.random.default_rng(0)
-    pool = (rng.random(1 << 28, dtype=np.float32) * 2 - 1) * np.float32(0.02 * 3 ** 0.5)
-
-    def tensor(shape):
-        n = int(np.prod(shape))
-        if n <= pool.size:
-            o = int(rng.integers(0, pool.size - n + 1))
-            return pool[o:o + n].reshape(shape)
-        return np.resize(pool, n).reshape(shape)
-
-    t_up = time.perf_counter()
-    ctx.upload(0, l3hip.W_EMBED, np.resize(pool * np.float32(50.0), VS * D).reshape(VS, D))
-    for i in range(args.n_layers):
-        for kind, shape in ((l3hip.W_Q, (H * HD, D)), (l3hip.W_K, (KVH * HD, D)), (l3hip.W_V, (KVH * HD, D)),
-                            (l3hip.W_O, (D, H * HD)), (l3hip.W_GATE, (FD, D)), (l3hip.W_UP, (FD, D)),
-                            (l3hip.W_DOWN, (D, FD))):
-            ctx.upload(i, kind, tensor(shape))
-        ctx.upload(i, l3hip.W_ATTN_NORM, np.ones(D, np.float32))
-        ctx.upload(i, l3hip.W_FFN_NORM, np.ones(D, np.float32))
-    ctx.upload(0, l3hip.W_FINAL_NORM, np.ones(D, np.float32))
-    ctx.upload(0, l3hip.W_LM_HEAD, tensor((VS, D)))
-    ctx.finalize()
     t_up = time.perf_counter() - t_up
     ids = rng.integers(0, VS, (B, L)).astype(np.int32)
     ids_dev = ctx.alloc(ids.nbytes)
@@ -414,7 +475,14 @@ def main():
     ap.add_argument("--rccl", action="store_true",
                     help="communicator, gather and self-check even at N=1 (rehearses the N>1 path "
                          "under torch.distributed.run --nproc-per-node 1)")
+    ap.add_argument("--spawn", action="store_true",
+                    help="start the rank processes here even at N=1 (rehearses the launcher-free "
+                         "N>1 path; N>1 without WORLD_SIZE spawns anyway)")
     a = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.spawn):
+        # no launcher: this process only starts the ranks (nothing here has touched the GPU)
+        argv = [x for x in sys.argv[1:] if x != "--spawn"]
+        raise SystemExit(spawn_ranks(a.gpus, argv))
     if a.workload == "c5":
         return bench_c5(a)
     if a.workload == "c5cpu":

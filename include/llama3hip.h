@@ -116,9 +116,13 @@ int l3_set_batch_split(l3_ctx* ctx, int32_t parts, int64_t min_tokens);
 /* Last layer of a model forward (extension; default on, env L3_LAST_LAYER_ALL_ROWS=1 turns it
  * off): only each sequence's last position reaches the logits (llama3.py:304), so the last
  * block runs its QKV GEMM on every position (the KV cache gets every slot, as the reference's)
- * and its attention, O-proj and FFN on the last position only.  Logits and caches are the
- * full block's (the attention of that row runs on the decode kernel: fp32 rounding differs
- * from the prefill kernel's by ~1e-7).  all_rows != 0: every position through the whole block. */
+ * and its attention, O-proj and FFN on the last position only.  The caches are the full
+ * block's, bit for bit.  The logits equal the all-rows forward's to fp32 rounding, not bit for
+ * bit: past 256 rows (B*L) the pruned row's attention runs on the decode kernel (K / V-only QKV
+ * for every row plus a B-row q GEMM), at <= 256 rows on the prefill kernel over each sequence's
+ * last q-blocks; the small GEMMs after it take the skinny MFMA kernel at M = B either way
+ * (tests: <= 1e-5 against the all-rows logits, C smoke 1e-4).  all_rows != 0: every position
+ * through the whole block. */
 int l3_set_last_layer_rows(l3_ctx* ctx, int32_t all_rows);
 /* Same with device-resident ids (int32 [B, L]) and logits ([B, VS]); async. */
 int l3_forward_dev(l3_ctx* ctx, const int32_t* ids_dev, int32_t B, int32_t L,
@@ -195,8 +199,12 @@ int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
  * the previous l3_greedy_step_host returned) answered. */
 int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits);
 /* Lazy greedy decode runs up to 16 steps ahead of the caller on the device (undone if the
- * caller leaves the schedule, so results are unchanged); no step at position >= end_pos is run
- * ahead (Llama.generate passes its max_new_tokens, llama3.py:312).  end_pos <= 0: no horizon. */
+ * caller leaves the schedule, so results are unchanged), and at most ~4 ms of decode work by
+ * the measured step time: a caller that stops early (EOS, an abandoned generator) or makes any
+ * other call first waits for at most that much queued work plus one step (stories15M: 16 steps
+ * ≈ 1.6 ms; Llama-3-8B shape at ~5 ms per step: no run-ahead).  No step at position >= end_pos
+ * is run ahead (Llama.generate passes its max_new_tokens, llama3.py:312).  end_pos <= 0: no
+ * horizon.  Env L3_DECODE_SPECULATE=0 turns run-ahead off. */
 int l3_set_decode_horizon(l3_ctx* ctx, int32_t end_pos);
 
 /* ---- multi-GPU: batch-sharded prefill + RCCL logits gather (xGMI) -------- */
@@ -205,10 +213,13 @@ int l3_comm_unique_id(uint8_t id_out[128]);
 int l3_comm_init(l3_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 /* Gather each rank's logits rows [rows_r, VS] (device) into root's dst_dev
  * [sum rows, VS] in rank order; rows_per_rank has nranks entries.  Async, on
- * the context's comm stream after the work queued so far: the next
- * l3_forward_dev overlaps it with its layers and waits for it only before its
- * lm_head (the writer of src); every other call (l3_d2h of dst_dev,
- * l3_synchronize, ...) waits for it first. */
+ * the context stream: it runs after the forward that wrote src and before
+ * whatever is queued next (the next l3_forward_dev starts once it is done; an
+ * l3_d2h of dst_dev or l3_synchronize sees the gathered rows).  Calls of one
+ * step must be made in the same order on every rank (RCCL point-to-point:
+ * one grouped ncclRecv per peer on the root, one ncclSend per non-root rank).
+ * Env L3_COMM_MODE=0 selects the older overlapped form (comm stream ordered by
+ * events, for A/B only; measured slower, DESIGN.md Multi-GPU). */
 int l3_comm_gather_logits(l3_ctx* ctx, const float* src_dev, float* dst_dev,
                           const int64_t* rows_per_rank, int32_t root);
 /* Greedy ids only (SURVEY 8(e) option): argmax of each rank's logits rows

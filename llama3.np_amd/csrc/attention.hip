@@ -1,6 +1,4 @@
 // Fused causal attention dispatch (kernel template and design notes: attn_kernel.h).
-#include <cstdlib>
-
 #include "attn_kernel.h"
 
 namespace l3 {
@@ -9,18 +7,6 @@ template <int HD, int QBW, int G, int KT>
 static hipError_t launch(const AttnArgs& a, hipStream_t s) {
     constexpr int QW = 16 * QBW * (4 / G);
     dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B), block(256);
-    // DEFER (attn_kernel.h), A/B only (L3_ATTN_DEFER=1): HD 48, one KV head per workgroup,
-    // 256-query workgroups over whole 256-multiple prompts from position 0.  Alone it is faster
-    // (C3 attention 117.3 -> 114.1 us, 54.1 % of peak), but its 75 KB of LDS leaves less room
-    // beside the other batch part's GEMM blocks: the split C3 step went 6.96 -> 7.01 ms in three
-    // interleaved A/B pairs (profiles/r02_attn_defer.log, r02_attn_defer_ab.log), so it is off
-    if constexpr (HD == 48 && G == 1 && QW == 256 && KT == 64) {
-        static const int defer = [] { const char* e = getenv("L3_ATTN_DEFER"); return e ? atoi(e) : 0; }();
-        if (defer && a.start_pos == 0 && !a.pos_dev && a.L % QW == 0) {
-            hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT, 0, true>), grid, block, 0, s, a);
-            return hipGetLastError();
-        }
-    }
     hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, block, 0, s, a);
     return hipGetLastError();
 }

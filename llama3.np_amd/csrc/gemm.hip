@@ -208,6 +208,9 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         }
     }
     if (gemm_is_gemv(a)) {
+        // GemmArgs::col_base (a K / V-only QKV) is honoured by the skinny and tiled epilogues
+        // only: the GEMV would write the K / V columns as q
+        if (a.col_base) return hipErrorInvalidValue;
         switch (epi) {
             case EPI_SWIGLU: return launch_gemv<EPI_SWIGLU>(a, s);
             case EPI_QKV: return launch_gemv<EPI_QKV>(a, s);
@@ -216,7 +219,7 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
             default: return hipErrorInvalidValue;
         }
     }
-    if (a.ws) {
+    if (a.ws && !a.col_base) {  // splitk_finish_kernel's QKV epilogue has no col_base either
         const hipError_t e = launch_split(epi, a, s);
         if (e != hipErrorNotReady) return e;
     }

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <chrono>
 #include <deque>
 #include <vector>
 
@@ -159,7 +160,13 @@ struct l3_ctx {
     // device; each step's ids land in spec_hist by position), so the GPU keeps running while the
     // host yields.  Every captured QKV append first keeps the slot it overwrites in kv_bak; a call
     // that does not continue the schedule restores the slots of every step not yet handed out.
+    // The queue is bounded by steps (SPEC_AHEAD) and by time: at most SPEC_BUDGET_US of queued
+    // decode work, by the measured step time (step_us), so a caller that leaves the schedule
+    // (EOS, an abandoned generator) waits at most about that long for work nobody asked for —
+    // 16 steps at stories15M's 0.1 ms, none at the Llama-3-8B shape's 5 ms per step.
     static constexpr int SPEC_AHEAD = 16;
+    static constexpr double SPEC_BUDGET_US = 4000.0;
+    double step_us = 0.0;            // decode step time, host wall clock of synced steps (EMA)
     float* kv_bak = nullptr;         // [n_layers][KV_BAK_SLOTS][2: k, v][8][KVH][HD]
     bool bak_capture = false;        // run_layer: QKV launches keep the overwritten slot
     bool dec_bak = false;            // the captured single-step graph keeps it
@@ -912,6 +919,22 @@ static bool speculation_on() {
     return on;
 }
 
+// how many decode steps may be queued ahead: SPEC_AHEAD, fewer when that much work would
+// exceed SPEC_BUDGET_US at the measured step time (0 before any step was timed)
+static int spec_ahead(const l3_ctx* c) {
+    if (c->step_us <= 0.0) return 0;
+    const double n = l3_ctx::SPEC_BUDGET_US / c->step_us;
+    return n >= l3_ctx::SPEC_AHEAD ? l3_ctx::SPEC_AHEAD : (int)n;
+}
+
+static void note_step_time(l3_ctx* c, double us) {
+    c->step_us = c->step_us > 0.0 ? 0.75 * c->step_us + 0.25 * us : us;
+}
+
+static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // B <= 8 with run-ahead on: every QKV of a step runs on the GEMV, whose epilogue keeps the
 // overwritten slot (GemmArgs::kv_bak)
 static int bak_wanted(l3_ctx* c, int B, bool* bak) {
@@ -1001,13 +1024,14 @@ static int speculate(l3_ctx* c, int B) {
             c->spec_hist_armed = true;
         }
     }
-    const int n = c->dec_n_bak && c->dec_n_B == B ? c->dec_n : 1;
+    const int ahead = spec_ahead(c);
+    const int n = c->dec_n_bak && c->dec_n_B == B && c->dec_n <= ahead ? c->dec_n : 1;
     while (c->spec_end < limit) {
         // whole n-step graphs (the queue refills by n once n steps have been handed out, so it
-        // holds SPEC_AHEAD - n .. SPEC_AHEAD steps); single steps only for the tail before the
-        // horizon
+        // holds ahead - n .. ahead steps); single steps for the tail before the horizon, or when
+        // the time budget allows fewer than n
         const int k = n > 1 && limit - c->spec_end >= n ? n : 1;
-        if (c->spec_end - c->spec_base + k > l3_ctx::SPEC_AHEAD) break;
+        if (c->spec_end - c->spec_base + k > ahead) break;
         HIP_TRY(hipGraphLaunch(k > 1 ? c->dec_exec_n : c->dec_exec, c->stream));
         HIP_TRY(hipMemcpyAsync(c->spec_ids + (size_t)c->spec_end * B, c->spec_hist + (size_t)c->spec_end * B,
                                (size_t)k * B * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1089,9 +1113,11 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
                   c->dec_pos_mirror == start_pos && (int)c->dec_last.size() == B && !c->timing;
     for (int i = 0; replay && i < B; ++i) replay = c->dec_last[(size_t)i] == ids_host[i];
     if (replay) {
+        const double t0 = now_us();
         HIP_TRY(hipGraphLaunch(c->dec_exec, c->stream));
         HIP_TRY(hipMemcpyAsync(c->dec_host, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        note_step_time(c, now_us() - t0);
         for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
         c->dec_last.assign(next_ids_host, next_ids_host + B);
         c->dec_pos_mirror = start_pos + 1;
@@ -1099,6 +1125,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
         return speculate(c, B);
     }
     c->dec_pos_mirror = -1;
+    const double t_eager = now_us();
     if (upload_ids(c, ids_host, (int64_t)B * L)) return 1;
     if (forward_dev(c, c->ids, B, L, start_pos, c->logits)) return 1;
     if (timed(c, L3_K_ARGMAX, [&] { return launch_greedy_argmax(c, B, nullptr); }))
@@ -1108,6 +1135,9 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
         HIP_TRY(hipMemcpyAsync(logits_host, c->logits, (int64_t)B * c->d.vocab_size * 4,
                                hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    // an eager decode step (per-kernel launches: an upper bound of the replayed step) seeds the
+    // run-ahead budget's step time; prefill calls (L > 1) do not
+    if (L == 1) note_step_time(c, now_us() - t_eager);
     for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
     // L3_DECODE_GRAPH=0 keeps every step eager (rocprofv3 kernel tracing does not survive
     // stream capture in this ROCm build)

@@ -143,13 +143,21 @@ class PinnedPool:
     rate into such a buffer instead of through a pageable bounce.  The array owns its
     block through a ctypes buffer object; once the array and every view of it are gone the
     block returns to a free list and the next call of the same size reuses it (at most
-    ``keep`` free blocks are kept, the rest are freed)."""
+    ``keep`` free blocks are kept, the rest are freed).
 
-    def __init__(self, keep: int = 4):
+    Bounded: at most ``max_bytes`` are page-locked at once (blocks handed out plus cached); a
+    request beyond that, or smaller than ``min_bytes`` (where pinning buys nothing), gets an
+    ordinary ``np.empty`` array instead, so a caller that keeps many results never pins
+    unbounded host memory."""
+
+    def __init__(self, keep: int = 4, max_bytes: int = 1 << 30, min_bytes: int = 1 << 16):
         import threading
 
         self.keep = keep
+        self.max_bytes = max_bytes
+        self.min_bytes = min_bytes
         self._free = {}  # nbytes -> [address]
+        self._pinned = 0  # bytes page-locked now: handed out + cached
         self._lock = threading.Lock()
 
     def empty(self, shape, dtype) -> np.ndarray:
@@ -158,12 +166,23 @@ class PinnedPool:
         dtype = np.dtype(dtype)
         n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
         nb = max(n, 64)
+        if nb < self.min_bytes:
+            return np.empty(shape, dtype)
         with self._lock:
             blocks = self._free.get(nb)
             addr = blocks.pop() if blocks else None
+            if addr is None:
+                if self._pinned + nb > self.max_bytes:
+                    return np.empty(shape, dtype)
+                self._pinned += nb  # reserved before the allocation
         if addr is None:
             p = ctypes.c_void_p()
-            check(lib().l3_host_alloc(nb, ctypes.byref(p)))
+            try:
+                check(lib().l3_host_alloc(nb, ctypes.byref(p)))
+            except Exception:
+                with self._lock:
+                    self._pinned -= nb
+                raise
             addr = p.value
         holder = (ctypes.c_char * nb).from_address(addr)
         weakref.finalize(holder, self._release, addr, nb)
@@ -175,15 +194,21 @@ class PinnedPool:
             if len(blocks) < self.keep:
                 blocks.append(addr)
                 return
+            self._pinned -= nb
         lib().l3_host_free(addr)
+
+    @property
+    def pinned_bytes(self) -> int:
+        return self._pinned
 
     def clear(self) -> None:
         """Free every cached block (arrays still alive are freed when dropped)."""
         with self._lock:
-            blocks = [a for v in self._free.values() for a in v]
+            blocks = [(a, nb) for nb, v in self._free.items() for a in v]
             self._free.clear()
             self.keep = 0
-        for addr in blocks:
+            self._pinned -= sum(nb for _, nb in blocks)
+        for addr, _ in blocks:
             lib().l3_host_free(addr)
 
 
@@ -424,7 +449,11 @@ def launch_key() -> str:
     """Key of the RCCL-id hand-off file: equal on every rank of one launch, different for every
     launch — torchrun's run id (TORCHELASTIC_RUN_ID; "none" under the default static rendezvous,
     so not unique alone), the launcher's pid (torchrun's agent is the parent of every rank it
-    starts) and MASTER_PORT."""
+    starts) and MASTER_PORT.  A launcher that sets L3_LAUNCH_KEY (bench.py's spawn_ranks) names
+    the launch itself."""
+    own = os.environ.get("L3_LAUNCH_KEY")
+    if own:
+        return own
     run = os.environ.get("TORCHELASTIC_RUN_ID") or "local"
     return f"{run}_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}"
 

@@ -35,14 +35,14 @@ import os
 import sys
 import time
 import zipfile
-from typing import Iterator, Optional
+from typing import Iterator, Mapping, Optional
 
 import numpy as np
 
 import l3hip
 from config import ModelArgs
 from tokenizer import Tokenizer
-from utils import RecyclingAlloc, StreamingNpz, load_parameters
+from utils import RecyclingAlloc, StreamingNpz, load_parameters, weight_names
 
 # .npz reader (A/B: tools/load_probe.py): "threads" — utils.StreamingNpz into ordinary arrays,
 # recycled when host copies are not kept (default), "pinned" — into recycled page-locked buffers
@@ -273,18 +273,28 @@ class Llama:
         ``keep_host_weights=False`` every ``.npz`` member is read, uploaded to HBM and
         dropped before the next is read (NumPy's NpzFile reads members lazily), so host
         memory peaks at one tensor instead of the whole checkpoint (32 GB for the
-        Llama-3-8B shape); the reference-style host attributes then hold placeholders."""
+        Llama-3-8B shape); the reference-style host attributes then hold placeholders.
+        ``model_path`` may also be a mapping of the ``.npz`` keys to arrays (what
+        ``load_parameters`` returns; extension) — uploaded as given, no file read."""
         self.args = args
         keep = keep_host_weights
         pool = None
-        if _NPZ_READER == "npzfile" or not zipfile.is_zipfile(model_path):
+        if isinstance(model_path, Mapping):
+            weight = model_path
+        elif _NPZ_READER == "npzfile" or not zipfile.is_zipfile(model_path):
             weight = load_parameters(model_path)
         elif keep:  # the arrays NpzFile would give, read by 8 threads without the zip CRC pass
             weight = StreamingNpz(model_path, np.empty)
         else:  # streaming: each member's buffer recycled once uploaded (gate, up and down of a
             # layer share a size and live together: 3 per size)
-            pool = l3hip.PinnedPool(keep=3) if _NPZ_READER == "pinned" else RecyclingAlloc(keep=3)
+            pool = l3hip.PinnedPool(keep=3, max_bytes=1 << 36) if _NPZ_READER == "pinned" else RecyclingAlloc(keep=3)
             weight = StreamingNpz(model_path, pool.empty if _NPZ_READER == "pinned" else pool)
+        # every tensor the forward reads, checked before anything is allocated (the reference
+        # fails late, with AttributeError on None.T, llama3.py:133-136)
+        missing = [n for n in weight_names(args.n_layers) if n not in weight]
+        if missing:
+            raise KeyError(f"missing weight(s) {missing[:4]}{' ...' if len(missing) > 4 else ''} "
+                           f"({len(missing)} of {len(weight_names(args.n_layers))})")
         self.freqs_cos, self.freqs_sin = compute_cos_sin_cache(args.dim // args.n_heads,
                                                                args.max_seq_len)
         hidden = weight.get("model.layers.0.mlp.gate_proj.weight").shape[0]

@@ -19,7 +19,7 @@ made from the same weights.
 """
 
 import hashlib
-from typing import Dict
+from typing import Dict, Optional
 
 import numpy as np
 
@@ -55,6 +55,45 @@ def make_weights(args: ModelArgs, hidden_dim: int, seed: int = 0,
         w[p + "post_attention_layernorm.weight"] = np.ones(D, np.float32)
     w["model.norm.weight"] = np.ones(D, np.float32)
     w["lm_head.weight"] = normal((args.vocab_size, D), cfg["std"] * cfg["lm_scale"])
+    return w
+
+
+def pool_weights(args: ModelArgs, hidden_dim: int, seed: int = 0, pool_floats: int = 1 << 28,
+                 std: float = 0.02, emb_scale: float = 50.0,
+                 rng: Optional[np.random.Generator] = None) -> Dict[str, np.ndarray]:
+    """Weights for shapes too large to draw tensor by tensor (the 32-layer Llama-3-8B shape is
+    8.5G floats): one uniform pool of ``pool_floats`` values with standard deviation ``std``,
+    every projection a contiguous view of it at a random offset (no copy), the embedding the
+    pool scaled by ``emb_scale`` and tiled to [VS, D] (std ~1 at the default), norms = 1.  Same
+    keys and [out, in] layouts as ``make_weights``; the draw order is fixed, so a seed gives the
+    same weights here and in bench.py's Llama-3-shape runs (which pass their own ``rng`` and
+    draw their token ids from it afterwards)."""
+    rng = np.random.default_rng(seed) if rng is None else rng
+    pool = (rng.random(pool_floats, dtype=np.float32) * 2 - 1) * np.float32(std * 3 ** 0.5)
+    D, H, KVH, VS = args.dim, args.n_heads, args.kv_heads, args.vocab_size
+    HD = D // H
+
+    def view(shape):
+        n = int(np.prod(shape))
+        if n <= pool.size:
+            o = int(rng.integers(0, pool.size - n + 1))
+            return pool[o:o + n].reshape(shape)
+        return np.resize(pool, n).reshape(shape)
+
+    w = {"model.embed_tokens.weight": np.resize(pool * np.float32(emb_scale), VS * D).reshape(VS, D)}
+    for i in range(args.n_layers):
+        p = f"model.layers.{i}."
+        w[p + "self_attn.q_proj.weight"] = view((H * HD, D))
+        w[p + "self_attn.k_proj.weight"] = view((KVH * HD, D))
+        w[p + "self_attn.v_proj.weight"] = view((KVH * HD, D))
+        w[p + "self_attn.o_proj.weight"] = view((D, H * HD))
+        w[p + "mlp.gate_proj.weight"] = view((hidden_dim, D))
+        w[p + "mlp.up_proj.weight"] = view((hidden_dim, D))
+        w[p + "mlp.down_proj.weight"] = view((D, hidden_dim))
+        w[p + "input_layernorm.weight"] = np.ones(D, np.float32)
+        w[p + "post_attention_layernorm.weight"] = np.ones(D, np.float32)
+    w["model.norm.weight"] = np.ones(D, np.float32)
+    w["lm_head.weight"] = view((VS, D))
     return w
 
 

@@ -5,12 +5,14 @@ mapping from HF-style tensor names to fp32 arrays stored ``[out, in]``
 row-major.  We return the same object (pickle stays disabled, NumPy's
 default), so ``weight.get(name)`` and ``weight[name]`` behave identically.
 
-``StreamingNpz`` (extension) is the streaming loader's reader: members go from the file
-straight into page-locked buffers for a DMA upload.
+``StreamingNpz`` (extension) is the ``.npz`` reader of ``Llama.__init__``: each member is
+read from the file by several ``preadv`` threads into a buffer from an allocator the caller
+passes — ordinary memory recycled per size (``RecyclingAlloc``) by default, page-locked
+buffers from ``l3hip.PinnedPool`` with ``L3_NPZ_READER=pinned``.
 
-``weight_names`` lists every key the forward pass reads; the device runtime
-uses it to fail early on a missing tensor instead of the reference's late
-``AttributeError`` on ``None.T`` (``llama3.py:133-136``).
+``weight_names`` lists every key the forward pass reads; ``Llama.__init__`` checks them all
+before it allocates anything, to fail early on a missing tensor instead of the reference's
+late ``AttributeError`` on ``None.T`` (``llama3.py:133-136``).
 """
 
 import ctypes
@@ -30,11 +32,13 @@ class StreamingNpz:
     """Extension: the streaming loader's view of an ``.npz``.
 
     ``get(name)`` reads one member straight from the file into a buffer made by
-    ``alloc(shape, dtype)`` — page-locked memory from ``l3hip.PinnedPool`` in
-    ``Llama(..., keep_host_weights=False)`` — so the H2D upload that follows is a DMA, and
-    the bytes are copied once (page cache -> pinned buffer, 32 MB ``preadv`` pieces on
-    ``threads`` threads at once) instead of three times (``NpzFile``: zip stream -> 256 KB
-    chunks -> array, with a CRC-32 pass, then the runtime's pageable bounce).  Stored
+    ``alloc(shape, dtype)`` — ``np.empty`` when host copies are kept, a ``RecyclingAlloc``
+    (ordinary memory, reused per size once uploaded) in ``Llama(..., keep_host_weights=False)``,
+    or page-locked ``l3hip.PinnedPool`` buffers with ``L3_NPZ_READER=pinned`` (a DMA upload;
+    measured slower overall) — and the bytes are copied once (page cache -> buffer,
+    32 MB ``preadv`` pieces on ``threads`` threads at once) instead of three times
+    (``NpzFile``: zip stream -> 256 KB chunks -> array, with a CRC-32 pass, then the runtime's
+    bounce).  Stored
     (uncompressed, as ``np.savez`` writes them) little-endian fp32 C-order members take this path; any other member (compressed,
     Fortran order, another dtype, a newer ``.npy`` header) is read by ``NpzFile`` as the
     reference's ``load_parameters`` would (same values either way; the fast path skips the

@@ -867,3 +867,70 @@ def test_host_path_pinned_logits(tmpdir_mod):
     np.testing.assert_array_equal(lc[:, 0, :], dev)
     ctx.free(ids_dev)
     ctx.free(out_dev)
+
+
+# ---- round 3: the Llama-3 shape at full depth ---------------------------------------------
+
+@pytest.mark.timeout(900)
+def test_c5_full_depth_32_layers_against_oracle():
+    """BASELINE configs[4] at its full depth: the reference runs every one of n_layers blocks
+    (llama3.py:277-278, 300-301), so all 32 Llama-3-8B-shaped layers (D 4096, GQA 32/8, HD 128,
+    FD 14336, VS 128256) against the oracle: B = 1, a 64-token prefill (split-K MFMA GEMMs,
+    prefill attention), then two decode steps at positions 65 and 66 across the decode hole at 64
+    (llama3.py:312-318; GEMV path).  Weights are views of one 1 GB uniform pool
+    (synth.pool_weights, as the bench's C5 weights), handed to Llama as a mapping, so neither side
+    needs 32 GB of fresh draws.  Bar: logits max-abs <= 1e-4 (north star), greedy ids equal."""
+    args = synth.llama3_shape(n_layers=32, max_batch_size=1, max_seq_len=128)
+    # a 2 GB pool: every tensor, the 525M-float lm_head included, is a view (a smaller pool is
+    # tiled, which repeats lm_head rows and ties their logits)
+    w = synth.pool_weights(args, synth.LLAMA3_HIDDEN, seed=0, pool_floats=1 << 29)
+    m = llama3.Llama(w, args)
+    ref = orc.OracleModel(w, args)
+    ids = np.random.default_rng(32).integers(0, args.vocab_size, (1, 64))
+    errs = {}
+    got, want = m(ids, 0), ref(ids, 0)
+    errs["prefill"] = float(np.max(np.abs(got.astype(np.float64) - want)))
+    nxt = want[:, -1, :].argmax(-1)[:, None]
+    assert int(got[0, -1].argmax()) == int(nxt[0, 0])
+    for pos in (65, 66):  # slot 64 is the decode hole
+        got, want = m(nxt, pos), ref(nxt, pos)
+        errs[f"decode@{pos}"] = float(np.max(np.abs(got.astype(np.float64) - want)))
+        assert int(got[0, -1].argmax()) == int(want[0, -1].argmax())
+        nxt = want[:, -1, :].argmax(-1)[:, None]
+    scale = float(np.max(np.abs(want)))
+    print(f"c5 32-layer max-abs logit errors {errs} (|logits| up to {scale:.2f})")
+    assert max(errs.values()) <= 1e-4, errs
+
+
+def test_pinned_pool_bounded():
+    """l3hip.PinnedPool pins at most max_bytes at once (handed out + cached); past the cap and
+    below min_bytes it hands out ordinary arrays, and released blocks free their bytes."""
+    import ctypes
+    import gc
+
+    pool = l3hip.PinnedPool(keep=1, max_bytes=3 << 20, min_bytes=1 << 16)
+
+    def pinned(a):  # the root owner of a pool array is its ctypes block
+        while isinstance(a, np.ndarray) and a.base is not None:
+            a = a.base
+        return isinstance(a, ctypes.Array)
+
+    small = pool.empty((1000,), np.float32)
+    assert not pinned(small) and pool.pinned_bytes == 0
+    a = pool.empty((1 << 18,), np.float32)  # 1 MB
+    b = pool.empty((1 << 18,), np.float32)
+    c = pool.empty((1 << 18,), np.float32)
+    assert pinned(a) and pinned(b) and pinned(c) and pool.pinned_bytes == 3 << 20
+    d = pool.empty((1 << 18,), np.float32)  # over the cap: ordinary memory
+    assert not pinned(d) and pool.pinned_bytes == 3 << 20
+    a[:] = 1.0
+    d[:] = 2.0
+    del a, b
+    gc.collect()
+    assert pool.pinned_bytes == 2 << 20  # one block cached (keep=1), one freed
+    e = pool.empty((1 << 18,), np.float32)  # the cached block again
+    assert pinned(e) and pool.pinned_bytes == 2 << 20
+    del c, e
+    gc.collect()
+    pool.clear()
+    assert pool.pinned_bytes == 0

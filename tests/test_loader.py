@@ -99,3 +99,19 @@ def test_recycling_alloc_reuses_dropped_blocks():
     pool.clear()
     del b, c
     assert not pool._free
+
+
+def test_llama_refuses_missing_weights_before_any_device_call():
+    """Llama.__init__ checks every tensor the forward reads (utils.weight_names) before it
+    creates a device context: a mapping without one raises KeyError here, on a CPU-only host
+    (the reference fails late, AttributeError on None.T, llama3.py:133-136)."""
+    import llama3
+    import synth
+    from utils import weight_names
+
+    args = synth.tiny(1)
+    w = synth.make_weights(args, synth.TINY_HIDDEN, seed=1)
+    assert sorted(weight_names(args.n_layers)) == sorted(w)
+    del w["model.layers.1.mlp.up_proj.weight"]
+    with pytest.raises(KeyError, match="up_proj"):
+        llama3.Llama(w, args)

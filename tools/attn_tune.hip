@@ -15,6 +15,7 @@
 #include "attn_variants.h"
 #include "attn_v3.h"
 #include "attn_resident.h"
+#include "attn_research.h"
 
 using namespace l3;
 
@@ -50,13 +51,13 @@ struct Variant {
     Variant{"defer<" #HD ",q" #QBW ",g" #G ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) { \
                 constexpr int QW = 16 * QBW * (4 / G);                                        \
                 dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
-                hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT, 0, true>), grid, dim3(256), 0, s, a); \
+                hipLaunchKernelGGL((attn_research_kernel<HD, QBW, G, KT, 0, true>), grid, dim3(256), 0, s, a); \
             }}
 
 #define AABL(ABL)                                                                             \
     Variant{"v1<48,q4,kt64> abl" #ABL, [](const AttnArgs& a, hipStream_t s) {                  \
                 dim3 grid((a.L + 255) / 256, a.H, a.B);                                        \
-                hipLaunchKernelGGL((attn_fwd_kernel<48, 4, 1, 64, ABL>), grid, dim3(256), 0, s, a); \
+                hipLaunchKernelGGL((attn_research_kernel<48, 4, 1, 64, ABL>), grid, dim3(256), 0, s, a); \
             }}
 
 #define AVAR3(QBW, KT, NS, WPE)                                                               \

@@ -22,7 +22,6 @@ for s in "$@"; do
     testsx) step tests 1200 python -m pytest tests -m gpu -q -x -rf --timeout 600 ;;
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --no-cpu-baseline ;;
-    defer[01]) L3_ATTN_DEFER=${s#defer} step $s 300 python bench.py --no-cpu-baseline ;;
     split[1-4]) L3_BATCH_SPLIT=${s#split} step $s 300 python bench.py --no-cpu-baseline ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1
@@ -85,6 +84,9 @@ for s in "$@"; do
     torchrun1p0) L3_COMM_PRIORITY=0 step torchrun1p0 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 1 --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
     torchrun1n) step torchrun1n 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
     torchrun1r) step torchrun1r 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29520 bench.py --gpus 1 --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
+    spawn1) step spawn1 300 python bench.py --spawn --rccl --steps 20 --warmup 3 --no-cpu-baseline ;;
+    c5deep) step c5deep 900 python -u -m pytest tests/test_gpu_parity.py -k c5_full_depth -x -v -s --timeout 900 --timeout-method thread ;;
+    testsv) step tests 1200 python -u -m pytest tests -m gpu -v -rfP --timeout 900 --timeout-method thread ;;
     benchr) step benchr 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
     benchrp0) L3_COMM_PRIORITY=0 step benchrp0 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
     benchrng) step benchrng 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl --no-step-gather ;;
