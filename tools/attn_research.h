@@ -10,6 +10,11 @@
 
 namespace l3 {
 
+// ABL & 512 (timing study, results correct): per-wave s_memtime stamps to g_attn_stamps,
+// 16 uint64 per wave: [0] entry, [1] after the prologue barrier, [2 + 2t] tile t's compute
+// done, [3 + 2t] after tile t's barrier (t < 4), [10] exit, [11] HW_REG_HW_ID, [12] XCC_ID
+__device__ unsigned long long* g_attn_stamps;
+
 // ABL: ablation bits for tools/attn_tune timing studies only (product launches use 0; results
 // are wrong with any bit set): 1 every tile full and unmasked for every block (no causal
 // structure), 2 p = s (no exp), 4 no K/V loads after tile 0, 8 no barrier in the tile loop,
@@ -51,6 +56,16 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
     __shared__ __attribute__((aligned(16))) float Vs[NS][KT][VSTR];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    unsigned long long* stp = nullptr;
+    if constexpr ((ABL & 512) != 0)
+        stp = g_attn_stamps + ((((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + wid) * 16;
+    auto stamp = [&](int i) {
+        if constexpr ((ABL & 512) != 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (lane == 0) stp[i] = t;
+        }
+    };
+    stamp(0);
     const int g = wid % G, part = wid / G;
     const int qt = blockIdx.x, b = blockIdx.z;
     const int h = blockIdx.y * G + g;
@@ -130,6 +145,7 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
         if (ntiles > 1) gload(1);  // set A holds tile 1
     }
     __syncthreads();
+    stamp(1);
     int cur = 0;  // slot of this tile (tile % NS)
     for (int tile = 0; tile < ntiles; ++tile) {
         const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
@@ -249,6 +265,7 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
                     qblock_tile(j, qblock_first, qmax_abs, cur, k0, std::integral_constant<bool, true>{});
             }
         }
+        if (tile < 4) stamp(2 + 2 * tile);
         if constexpr ((ABL & 32) != 0) {
             if (tile + 1 < ntiles) {
                 if (tile & 1) sstore_from(nxt, rk2, rv2);
@@ -258,6 +275,7 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
             sstore(nxt);
         }
         if constexpr (!(ABL & 8)) __syncthreads();
+        if (tile < 4) stamp(3 + 2 * tile);
         cur = nxt;
     }
 
@@ -273,6 +291,13 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
 #pragma unroll
             for (int dg = 0; dg < ND; ++dg)
                 *reinterpret_cast<f32x4*>(dst + dg * 16) = o[j][dg] * inv;
+        }
+    }
+    stamp(10);
+    if constexpr ((ABL & 512) != 0) {
+        if (lane == 0) {
+            stp[11] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+            stp[12] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
         }
     }
 }

@@ -16,6 +16,7 @@
 #include "attn_v3.h"
 #include "attn_resident.h"
 #include "attn_research.h"
+#include "attn_pair.h"
 
 using namespace l3;
 
@@ -38,6 +39,13 @@ struct Variant {
                 constexpr int QW = 16 * QBW * (4 / G);                                        \
                 dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, dim3(256), 0, s, a); \
+            }}
+
+#define APAIR(HD, QBW, KT, MIR)                                                               \
+    Variant{"pair<" #HD ",q" #QBW ",kt" #KT ",mirror" #MIR ">", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * 4;                                              \
+                dim3 grid((a.L + QW - 1) / QW, a.H / 2, a.B);                                 \
+                hipLaunchKernelGGL((attn_pair_kernel<HD, QBW, KT, MIR>), grid, dim3(512), 0, s, a); \
             }}
 
 #define AVAR2(HD, QBW, G, KT, WPE)                                                            \
@@ -154,8 +162,56 @@ static void run(const char* label, int B, int L, int H, int KVH, int HD, std::ve
     CK(hipFree(q)); CK(hipFree(k)); CK(hipFree(v)); CK(hipFree(o));
 }
 
+// Per-wave s_memtime stamps of the C3 launch (research kernel with ABL 512: same code as the
+// product kernel plus the stamps), after `warm` warm-up launches; raw dump for
+// tools/attn_stamps.py: [n_waves][16] uint64 (layout in attn_research.h)
+static void stamps(const char* path, int warm) {
+    const int B = 256, L = 256, H = 6, HD = 48;
+    const size_t nq = (size_t)B * L * H * HD;
+    std::vector<float> hq(nq);
+    fill(hq, -1.f, 1.f, 1);
+    float *q, *k, *v, *o;
+    CK(hipMalloc(&q, nq * 4)); CK(hipMalloc(&k, nq * 4)); CK(hipMalloc(&v, nq * 4)); CK(hipMalloc(&o, nq * 4));
+    CK(hipMemcpy(q, hq.data(), nq * 4, hipMemcpyHostToDevice));
+    fill(hq, -1.f, 1.f, 2);
+    CK(hipMemcpy(k, hq.data(), nq * 4, hipMemcpyHostToDevice));
+    fill(hq, -1.f, 1.f, 3);
+    CK(hipMemcpy(v, hq.data(), nq * 4, hipMemcpyHostToDevice));
+    AttnArgs a{};
+    a.q = q; a.cache_k = k; a.cache_v = v; a.out = o;
+    a.B = B; a.L = L; a.start_pos = 0; a.H = H; a.KVH = H; a.HD = HD; a.Smax = L;
+    dim3 grid(1, H, B);
+    const size_t nst = (size_t)B * H * 4 * 16;
+    unsigned long long* st;
+    CK(hipMalloc(&st, nst * 8));
+    CK(hipMemset(st, 0, nst * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &st, sizeof(st)));
+    for (int i = 0; i <= warm; ++i)
+        hipLaunchKernelGGL((attn_research_kernel<48, 4, 1, 64, 512>), grid, dim3(256), 0, 0, a);
+    CK(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(nst);
+    CK(hipMemcpy(h.data(), st, nst * 8, hipMemcpyDeviceToHost));
+    FILE* f = fopen(path, "wb");
+    fwrite(h.data(), 8, nst, f);
+    fclose(f);
+    printf("stamps: %zu waves -> %s\n", nst / 16, path);
+    CK(hipFree(q)); CK(hipFree(k)); CK(hipFree(v)); CK(hipFree(o)); CK(hipFree(st));
+}
+
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
+    if (argc > 3 && std::string(argv[3]) == "pair") {  // two items per 8-wave workgroup
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), APAIR(48, 4, 64, true), APAIR(48, 4, 64, false),
+                                  AVAR(48, 4, 1, 64), APAIR(48, 4, 64, true)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "stamps") {
+        stamps(argc > 4 ? argv[4] : "gpurun_out/attn_stamps.bin", rounds);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "c3") {  // the product C3 kernel alone (PMC passes)
         run("stories15M C3", 256, 256, 6, 6, 48, {AVAR(48, 4, 1, 64)}, rounds, iters);
         return 0;
