@@ -29,8 +29,8 @@ static hipError_t launch_split_cfg(int epi, GemmArgs a, hipStream_t s) {
     const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     const int nk = a.K / BK;
     const int64_t need_per = (int64_t)a.M * a.N + a.M;  // floats per slice
-    static const int target = [] { const char* e = getenv("L3_SPLITK_BLOCKS"); return e ? atoi(e) : 1024; }();
-    static const int min_kt = [] { const char* e = getenv("L3_SPLITK_MINKT"); return e ? atoi(e) : 8; }();
+    static const int target = env_knob("L3_SPLITK_BLOCKS", 1024);
+    static const int min_kt = env_knob("L3_SPLITK_MINKT", 8);
     int S = 1;
     while (S < 16 && tiles * S < target && nk % (2 * S) == 0 && nk / (2 * S) >= min_kt &&
            2 * S * need_per <= a.ws_cap)
@@ -53,8 +53,8 @@ static hipError_t launch_split_cfg(int epi, GemmArgs a, hipStream_t s) {
 
 // L3_SPLITK=0: off (A/B); L3_SPLITK_CFG picks the slice tile (tuning)
 static hipError_t launch_split(int epi, const GemmArgs& a, hipStream_t s) {
-    static const int on = [] { const char* e = getenv("L3_SPLITK"); return e ? atoi(e) : 1; }();
-    static const int cfg = [] { const char* e = getenv("L3_SPLITK_CFG"); return e ? atoi(e) : 0; }();
+    static const int on = env_knob("L3_SPLITK", 1);
+    static const int cfg = env_knob("L3_SPLITK_CFG", 0);
     if (!on || !a.ws || a.M <= 8 || a.M > 256 || a.K < 2048 || a.K % 32 != 0) return hipErrorNotReady;
     switch (cfg) {
         case 1: return launch_split_cfg<2, 2, 4, 4, 16, 2>(epi, a, s);
@@ -81,7 +81,7 @@ static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
 // non-temporal W loads for the one-row GEMV over a weight larger than the caches would keep
 // (>= 64 MB: the Llama-3-shape decode; gemv_kernel NT); L3_GEMV_NT=0 turns them off (A/B)
 static bool gemv_nt(const GemmArgs& a) {
-    static const int on = [] { const char* e = getenv("L3_GEMV_NT"); return e ? atoi(e) : 1; }();
+    static const int on = env_knob("L3_GEMV_NT", 1);
     return on && (int64_t)a.N * a.K * 4 >= ((int64_t)64 << 20);
 }
 
@@ -104,7 +104,7 @@ static hipError_t launch_gemv_parts(const GemmArgs& a, hipStream_t s) {
 // lanes per unit from K: ~5-8 float4 per lane per W row in one chunk at the stories15M sizes;
 // L3_GEMV_LPU=16/32/64 forces it (A/B tuning of the decode GEMVs)
 static int gemv_lpu(const GemmArgs& a) {
-    static const int force = [] { const char* e = getenv("L3_GEMV_LPU"); return e ? atoi(e) : 0; }();
+    static const int force = env_knob("L3_GEMV_LPU", 0);
     if (force == 16 || force == 32 || force == 64) return force;
     const int k4 = a.K / 4;
     return k4 <= 128 ? 16 : k4 <= 256 ? 32 : 64;
@@ -137,7 +137,7 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
     // trips (batched decode B = 64 0.355 -> 0.316, B = 256 0.548 -> 0.530 ms per step; 2-row
     // blocks 0.310 / 0.591; where the skinny MFMA kernel does not take them); a weight past the
     // caches keeps one block row up to M = 8 so it streams once.  L3_GEMV_MR caps it (tuning).
-    static const int env_cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 0; }();
+    static const int env_cap = env_knob("L3_GEMV_MR", 0);
     const bool small_w = (int64_t)a.N * a.K <= (int64_t)4 << 20;
     const int cap = env_cap ? env_cap : small_w ? 4 : 8;
     if (a.M <= 1 || cap == 1 || (small_w && a.M <= 8)) return launch_gemv_mr<EPI, 1>(a, s);
@@ -147,7 +147,7 @@ static hipError_t launch_gemv(const GemmArgs& a, hipStream_t s) {
 }
 
 bool gemv_direct(const GemmArgs& a) {
-    static const int cap = [] { const char* e = getenv("L3_GEMV_MR"); return e ? atoi(e) : 4; }();
+    static const int cap = env_knob("L3_GEMV_MR", 4);
     const bool small_w = (int64_t)a.N * a.K <= (int64_t)4 << 20;
     return gemm_is_gemv(a) && (a.M <= 1 || cap == 1 || (small_w && a.M <= 8));
 }
@@ -163,8 +163,8 @@ static hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
 }
 
 static bool use_skinny(const GemmArgs& a) {
-    static const int on = [] { const char* e = getenv("L3_SKINNY"); return e ? atoi(e) : 1; }();
-    static const int lo = [] { const char* e = getenv("L3_SKINNY_MIN"); return e ? atoi(e) : 9; }();
+    static const int on = env_knob("L3_SKINNY", 1);
+    static const int lo = env_knob("L3_SKINNY_MIN", 9);
     return on && a.M >= lo && a.M <= 256 && !a.kv_bak && !a.parts && !a.amax_part && a.K % 16 == 0;
 }
 

@@ -328,9 +328,9 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     l3_ctx* c = new l3_ctx();
     c->device = device;
     c->d = d;
-    if (const char* e = getenv("L3_LAST_LAYER_ALL_ROWS")) c->prune_last = atoi(e) == 0;
-    if (const char* e = getenv("L3_BATCH_SPLIT")) {  // default for new contexts
-        const int n = atoi(e);
+    c->prune_last = env_knob("L3_LAST_LAYER_ALL_ROWS", 0) == 0;
+    {  // batch-split default for new contexts
+        const int n = env_knob("L3_BATCH_SPLIT", c->split);
         c->split = n < 1 ? 1 : n > l3_ctx::MAX_PARTS ? l3_ctx::MAX_PARTS : n;
     }
     c->HD = HD;
@@ -676,7 +676,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     // so a step runs one launch per layer fewer (device loop 0.104 -> 0.101 ms/step; at B = 8
     // the redundant attention of the z blocks costs more than the launch: 0.129 -> 0.134, so
     // B > 1 keeps the O-proj GEMV).  L3_DECODE_FUSE_O=0 keeps it at B = 1 too (A/B).
-    static const bool fuse_env = [] { const char* e = getenv("L3_DECODE_FUSE_O"); return !e || e[0] != '0'; }();
+    static const bool fuse_env = env_knob("L3_DECODE_FUSE_O", 1) != 0;
     const bool fuse_o = fuse_env && L == 1 && c->oparts && c->hsum && b0 == 0 && T == 1 && D % 4 == 0 && c->HD % 16 == 0 &&
                         c->d.max_seq_len <= 8192 && gemv_direct(gu) && gemv_direct(dn);
     // causal attention over the cache
@@ -721,7 +721,7 @@ static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipSt
     GemmArgs lm = lm_head_args(c, B, L, logits_dev, b0);
     // batch 1 on the one-row GEMV: each block also leaves its (value, index) argmax, so a greedy
     // step's argmax reads those partials instead of the whole logits row (L3_LM_AMAX=0: off)
-    static const bool amax_env = [] { const char* e = getenv("L3_LM_AMAX"); return !e || e[0] != '0'; }();
+    static const bool amax_env = env_knob("L3_LM_AMAX", 1) != 0;
     c->amax_n = amax_env && b0 == 0 ? gemv_store_blocks(lm) : 0;
     if (c->amax_n) lm.amax_part = c->amax_part;
     return timed_on(c, L3_K_LMHEAD, s, [&] { return launch_gemm(EPI_STORE, lm, s); });
@@ -915,7 +915,7 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
 }
 
 static bool speculation_on() {
-    static const bool on = [] { const char* e = getenv("L3_DECODE_SPECULATE"); return !e || e[0] != '0'; }();
+    static const bool on = env_knob("L3_DECODE_SPECULATE", 1) != 0;
     return on;
 }
 
@@ -965,8 +965,7 @@ static int capture_decode_graph(l3_ctx* c, int B) {
 // of the single-step graph per token)
 static int decode_graph_steps() {
     static const int n = [] {
-        const char* e = getenv("L3_DECODE_GRAPH_STEPS");
-        const int v = e ? atoi(e) : 8;
+        const int v = env_knob("L3_DECODE_GRAPH_STEPS", 8);
         return v < 1 ? 1 : v > 64 ? 64 : v;
     }();
     return n;
@@ -1141,7 +1140,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
     for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
     // L3_DECODE_GRAPH=0 keeps every step eager (rocprofv3 kernel tracing does not survive
     // stream capture in this ROCm build)
-    static const bool graphs = [] { const char* e = getenv("L3_DECODE_GRAPH"); return !e || e[0] != '0'; }();
+    static const bool graphs = env_knob("L3_DECODE_GRAPH", 1) != 0;
     if (graphs && L == 1 && start_pos + 1 < c->d.max_seq_len) {
         // arm the device state for the next decode step (one position later) and capture
         const int next = start_pos + 1;
@@ -1539,8 +1538,7 @@ extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8
         int least = 0, greatest = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
         // L3_COMM_PRIORITY=0: normal priority (A/B of the queue placement)
-        const char* pe = getenv("L3_COMM_PRIORITY");
-        const int prio = (pe && pe[0] == '0') ? least : greatest;
+        const int prio = env_knob("L3_COMM_PRIORITY", 1) == 0 ? least : greatest;
         HIP_TRY(hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, prio));
         HIP_TRY(hipEventCreateWithFlags(&c->comm_fwd_ev, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->comm_done_ev, hipEventDisableTiming));
@@ -1579,7 +1577,7 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
     // it) measured 7.96 ms/step against 6.94 at world 1 on MI355X, and 7.97 still with the
     // comm stream left empty (mode 2: root's own rows on the context stream) — the event
     // hand-offs between the streams, not the transfer, cost the step (profiles/r02_comm_modes.md).
-    static const int mode = [] { const char* e = getenv("L3_COMM_MODE"); return e ? atoi(e) : 1; }();
+    static const int mode = env_knob("L3_COMM_MODE", 1);
     hipStream_t s = mode == 1 ? c->stream : c->comm_stream;
     hipStream_t self_s = mode == 0 ? s : c->stream;
     if (mode != 1) {
