@@ -17,6 +17,7 @@
 #include "attn_resident.h"
 #include "attn_research.h"
 #include "attn_pair.h"
+#include "attn_persist.h"
 
 using namespace l3;
 
@@ -39,6 +40,16 @@ struct Variant {
                 constexpr int QW = 16 * QBW * (4 / G);                                        \
                 dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, dim3(256), 0, s, a); \
+            }}
+
+// the product kernel on a multi-item grid: blocks resident at once = CAP (512 = 2 per CU)
+#define APERS(HD, QBW, G, KT, CAP)                                                            \
+    Variant{"persist<" #HD ",q" #QBW ",g" #G ",kt" #KT ",cap" #CAP ">", [](const AttnArgs& a, hipStream_t s) { \
+                launch_attn_persist<HD, QBW, G, KT>(a, s, CAP);                                    \
+            }}
+#define APERSQ(HD, QBW, G, KT, CAP)                                                           \
+    Variant{"persistq<" #HD ",q" #QBW ",g" #G ",kt" #KT ",cap" #CAP ">", [](const AttnArgs& a, hipStream_t s) { \
+                launch_attn_persist<HD, QBW, G, KT, true>(a, s, CAP);                              \
             }}
 
 #define APAIR(HD, QBW, KT, MIR)                                                               \
@@ -206,6 +217,18 @@ int main(int argc, char** argv) {
         run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
         run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
         run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "persist") {  // multi-item grids vs one block per item
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), APERS(48, 4, 1, 64, 512), APERSQ(48, 4, 1, 64, 512),
+                                  APERS(48, 4, 1, 64, 256), APERS(48, 4, 1, 64, 768), AVAR(48, 4, 1, 64),
+                                  APERS(48, 4, 1, 64, 512), APERSQ(48, 4, 1, 64, 512)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M C3 half batch (one part of the split)", 128, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M C4 on one GPU", 2048, 256, 6, 6, 48, v, 1, 3);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        std::vector<Variant> v5 = {AVAR(128, 1, 4, 32), APERS(128, 1, 4, 32, 512)};
+        run("Llama-3 shape B=4 L=2048", 4, 2048, 32, 8, 128, v5, 1, 2);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "stamps") {

@@ -46,6 +46,7 @@ for s in "$@"; do
     attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     attnstamps) step attnstamps 120 tools/attn_tune 3 1 stamps gpurun_out/attn_stamps.bin ;;
     attnpair) step attnpair 300 tools/attn_tune 5 10 pair ;;
+    attnpersist) step attnpersist 300 tools/attn_tune 5 10 persist ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
     floor) step floor 120 tools/launch_floor ;;
     hostprobe) step hostprobe 300 python tools/host_path_probe.py ;;
