@@ -213,13 +213,17 @@ int l3_comm_unique_id(uint8_t id_out[128]);
 int l3_comm_init(l3_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
 /* Gather each rank's logits rows [rows_r, VS] (device) into root's dst_dev
  * [sum rows, VS] in rank order; rows_per_rank has nranks entries.  Async, on
- * the context stream: it runs after the forward that wrote src and before
- * whatever is queued next (the next l3_forward_dev starts once it is done; an
- * l3_d2h of dst_dev or l3_synchronize sees the gathered rows).  Calls of one
+ * the context stream, after the forward that wrote src.  When the next call is
+ * l3_forward_dev with its batch split, that forward's second part starts from
+ * the point before the gather (its layers overlap the transfer), its first part
+ * runs after the gather, and every part's lm_head waits for it (it reads the
+ * rows the lm_head rewrites); any other entry point runs after the gather.  An
+ * l3_d2h of dst_dev or l3_synchronize sees the gathered rows.  Calls of one
  * step must be made in the same order on every rank (RCCL point-to-point:
  * one grouped ncclRecv per peer on the root, one ncclSend per non-root rank).
- * Env L3_COMM_MODE=0 selects the older overlapped form (comm stream ordered by
- * events, for A/B only; measured slower, DESIGN.md Multi-GPU). */
+ * Env L3_COMM_MODE (A/B only): 3 the form above (default), 1 the gather fully
+ * serialized on the context stream, 0 a comm stream ordered by events
+ * (measured slower, DESIGN.md Multi-GPU). */
 int l3_comm_gather_logits(l3_ctx* ctx, const float* src_dev, float* dst_dev,
                           const int64_t* rows_per_rank, int32_t root);
 /* Greedy ids only (SURVEY 8(e) option): argmax of each rank's logits rows

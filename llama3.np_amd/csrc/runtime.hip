@@ -131,13 +131,17 @@ struct l3_ctx {
     // rccl
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    // the logits gather runs on its own stream, so step k's transfer over xGMI overlaps step
-    // k+1's layers; the next lm_head (the writer of the gathered rows) waits for it, every
-    // other entry point joins it first (set_dev)
+    // comm stream of the A/B gather mode 0 (the default mode 3 gathers on stream, see
+    // l3_comm_gather_logits); the next lm_head (the writer of the gathered rows) waits for the
+    // gather, every other entry point joins it first (set_dev)
     hipStream_t comm_stream = nullptr;
     int32_t* gather_ids = nullptr;   // [maxB] this rank's argmax ids (l3_comm_gather_argmax)
     hipEvent_t comm_fwd_ev = nullptr, comm_done_ev = nullptr;
     bool gather_pending = false;
+    // mode 3 (L3_COMM_MODE): the gather was the last work queued on stream, and comm_fwd_ev marks
+    // the stream just before it — the next l3_forward_dev's second batch part starts from there,
+    // so its layers overlap the transfer (only that entry point keeps the flag: set_dev clears it)
+    bool gather_tail = false;
     // captured greedy decode step (llama3.py:316-320 as one hipGraph replay per token)
     int32_t* dec_ids = nullptr;      // [maxB] input ids of the next decode step (argmax output)
     DecState* dec_state = nullptr;   // device loop state: position, generate history
@@ -190,6 +194,7 @@ struct l3_ctx {
 // l3_forward_dev (which waits only before its lm_head) and the gather itself
 static int set_dev(l3_ctx* c, bool join = true) {
     HIP_TRY(hipSetDevice(c->device));
+    if (join) c->gather_tail = false;
     if (join && c->gather_pending) {
         HIP_TRY(hipStreamWaitEvent(c->stream, c->comm_done_ev, 0));
         c->gather_pending = false;
@@ -259,6 +264,7 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     const int64_t T = B * L;
     if (T <= c->ws_T && B <= c->ws_B) return 0;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->gather_tail = false;
     drop_decode_graph(c);  // the captured graph holds workspace pointers
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits);
     dfree(c->ids); dfree(c->amax); dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum);
@@ -764,9 +770,15 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
         st[p] = p ? c->aux[p - 1] : c->stream;
     }
     roctxRangePushA("l3.forward");
+    // a logits gather queued last on stream (mode 3): the other parts start from the point just
+    // before it, so their layers overlap the transfer; part 0 runs after it on stream, and every
+    // part's lm_head (the writer of the rows it reads) waits for it below (gather_pending)
+    const bool after_gather = c->gather_tail;
+    c->gather_tail = false;
     if (parts > 1) {  // the aux streams join the work queued so far on stream
-        HIP_TRY(hipEventRecord(c->fork_ev, c->stream));
-        for (int p = 1; p < parts; ++p) HIP_TRY(hipStreamWaitEvent(st[p], c->fork_ev, 0));
+        if (!after_gather) HIP_TRY(hipEventRecord(c->fork_ev, c->stream));
+        for (int p = 1; p < parts; ++p)
+            HIP_TRY(hipStreamWaitEvent(st[p], after_gather ? c->comm_fwd_ev : c->fork_ev, 0));
     }
     // the lm_head too runs per part when every part picks the unsplit batch's tile (then each
     // part's lm_head overlaps the other parts' last layer); otherwise once after the join
@@ -1055,6 +1067,7 @@ static int speculate(l3_ctx* c, int B) {
 static int spec_resolve(l3_ctx* c) {
     if (c->spec_q.empty()) return 0;
     HIP_TRY(hipSetDevice(c->device));
+    c->gather_tail = false;  // the restores below are queued after the gather
     const int KVH = c->d.n_kv_heads, HD = c->HD, n = c->spec_B * KVH * HD;
     for (int pos = c->spec_base; pos < c->spec_end; ++pos) {
         for (size_t li = 0; li < c->layers.size(); ++li) {
@@ -1571,19 +1584,25 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
     if (c->rank == root && !dst_dev) return fail("l3_comm_gather_logits: null destination on the root");
     if (set_dev(c, false)) return 1;
     const int64_t VS = c->d.vocab_size;
-    // Default (mode 1): on the context stream, after the forward that wrote src and before the
-    // next one — no cross-stream events.  The overlapped form (mode 0, L3_COMM_MODE=0: the
+    // Mode 1: on the context stream, after the forward that wrote src and before the next one —
+    // no cross-stream events, the transfer fully serialized.  The overlapped form (mode 0: the
     // transfer on the high-priority comm stream, ordered by events, the next lm_head waiting for
     // it) measured 7.96 ms/step against 6.94 at world 1 on MI355X, and 7.97 still with the
     // comm stream left empty (mode 2: root's own rows on the context stream) — the event
     // hand-offs between the streams, not the transfer, cost the step (profiles/r02_comm_modes.md).
-    static const int mode = env_knob("L3_COMM_MODE", 1);
-    hipStream_t s = mode == 1 ? c->stream : c->comm_stream;
+    //
+    // Mode 3 (default): on the context stream as mode 1, but bracketed by events so that the
+    // next l3_forward_dev's second batch part (aux stream) starts from the point before the
+    // gather: its layers overlap the transfer, part 0 follows the gather on the context stream,
+    // and both parts' lm_heads wait for its end (the rows it reads).  No comm stream; at world 1
+    // (a self-copy) 6.038 / 6.051 ms/step against mode 1's 6.044 / 6.058, gathered rows
+    // bit-exact (profiles/r03_comm_mode3_ab.log)
+    static const int mode = env_knob("L3_COMM_MODE", 3);
+    const bool on_ctx = mode == 1 || mode == 3;
+    hipStream_t s = on_ctx ? c->stream : c->comm_stream;
     hipStream_t self_s = mode == 0 ? s : c->stream;
-    if (mode != 1) {
-        HIP_TRY(hipEventRecord(c->comm_fwd_ev, c->stream));
-        HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->comm_fwd_ev, 0));
-    }
+    if (mode != 1) HIP_TRY(hipEventRecord(c->comm_fwd_ev, c->stream));
+    if (!on_ctx) HIP_TRY(hipStreamWaitEvent(c->comm_stream, c->comm_fwd_ev, 0));
     // RCCL has no native gather: root posts one recv per peer, peers one send, all in one
     // group so the point-to-point transfers run concurrently over the xGMI links.
     NCCL_TRY(ncclGroupStart());
@@ -1612,6 +1631,7 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
     if (mode != 1) {
         HIP_TRY(hipEventRecord(c->comm_done_ev, s));
         c->gather_pending = true;
+        c->gather_tail = mode == 3;
     }
     return 0;
 }

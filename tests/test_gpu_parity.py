@@ -333,8 +333,8 @@ def test_sharded_prefill_world1_rccl(tmpdir_mod):
 
 def test_gather_pipelined_forwards_world1(tmpdir_mod):
     """Forwards and gathers queued back to back on one logits buffer, as bench.py does: the
-    gather runs on the comm stream, overlapping the next forward's layers, and the next
-    lm_head waits for it.  Three forwards, two gathers into separate roots, then D2H — each
+    next forward's second batch part starts before the gather ends (overlapping it), part 0
+    and every lm_head wait for it.  Three forwards, two gathers into separate roots, then D2H — each
     holds its own step's logits, bit-identical to Llama.__call__ on the same rows, under each
     batch split."""
     args = synth.stories15m(16)
