@@ -14,7 +14,7 @@ static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
     const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, NS>),
-                       dim3((unsigned)tiles), dim3(256), 0, s, a);
+                       dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a);
     return hipGetLastError();
 }
 
@@ -38,7 +38,7 @@ static hipError_t launch_split_cfg(int epi, GemmArgs a, hipStream_t s) {
     if (S == 1) return hipErrorNotReady;  // not worth it: the caller runs the unsplit tiles
     a.splits = S;
     hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI_STORE, 2, false, BK, true, NS, true>),
-                       dim3((unsigned)(tiles * S)), dim3(256), 0, s, a);
+                       dim3((unsigned)(tiles * S)), dim3(64 * WM * WN), 0, s, a);
     if (const hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     const int64_t outs = (int64_t)a.M * (epi == EPI_SWIGLU ? a.N / 2 : a.N) / 4;
     const dim3 grid((unsigned)((outs + 255) / 256));

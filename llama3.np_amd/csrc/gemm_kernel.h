@@ -276,7 +276,8 @@ __device__ __forceinline__ void stamp_pair(unsigned long long* dst) {
     }
 
 // ---------------------------------------------------------------------------------------
-// Tiled kernel: 256 threads = 4 waves as WM x WN, wave tile (TM x 16) x (TN x 16).
+// Tiled kernel: 64 * WM * WN threads = WM x WN waves (the product tiles: 2 x 2), wave tile
+// (TM x 16) x (TN x 16).
 // counted wait for this wave's vector-memory ops (loads, stores and LDS-DMA alike, in order)
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -289,7 +290,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 // row sums of squares in p.ws (split_epilogue); splitk_finish_kernel sums the slices in order
 template <int WM, int WN, int TM, int TN, int EPI, int WAVES_PER_EU = 2, bool STAMP = false,
           int BK = 32, bool GLDS = true, int NS = 2, bool SPLIT = false>
-__global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
+__global__ void __launch_bounds__(64 * WM * WN, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p) {
+    constexpr int NW = WM * WN, NT = 64 * NW;  // waves, threads
     constexpr int BM = WM * TM * 16;
     constexpr int BN = WN * TN * 16;
     static_assert(BK == 16 || BK == 32, "BK must be 16 or 32");
@@ -297,7 +299,7 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     constexpr int Q = BK / 4;        // float4 per image row
     constexpr int RP = 256 / BK;     // image rows per 1 KB global_load_lds piece
     constexpr int A_F4 = BM * Q, B_F4 = BN * Q;
-    constexpr int A_IT = (A_F4 + 255) / 256, B_IT = (B_F4 + 255) / 256;
+    constexpr int A_IT = (A_F4 + NT - 1) / NT, B_IT = (B_F4 + NT - 1) / NT;
 
     // one LDS array: [NS][BM][BK] A image, then [NS][BN][BK] W image
     __shared__ __attribute__((aligned(16))) float smem[NS * (BM + BN) * BK];
@@ -322,28 +324,28 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     // rows past M / N are clamped (their outputs are never stored).
     // A-row source addresses are fixed for the tile: resolved once (a gathered embedding row
     // costs one index load per lane here, never inside the k-loop beside the DMA)
-    constexpr int A_PIECES = (BM / RP + 3) / 4;
+    constexpr int A_PIECES = (BM / RP + NW - 1) / NW;
     const float* a_src[A_PIECES];
 #pragma unroll
     for (int it = 0; it < A_PIECES; ++it) {
-        const int piece = wid + 4 * it, r = piece * RP + lane / Q;
+        const int piece = wid + NW * it, r = piece * RP + lane / Q;
         a_src[it] = a_row(p, min(m0 + r, p.M - 1)) + 4 * ((lane % Q) ^ lds_swz<BK>(r));
     }
     auto glds_tile = [&](int buf, int k0) {
         const int rl = lane / Q, pq = lane % Q;
 #pragma unroll
         for (int it = 0; it < A_PIECES; ++it) {
-            const int piece = wid + 4 * it;
-            if ((BM / RP) % 4 == 0 || piece < BM / RP) {
+            const int piece = wid + NW * it;
+            if ((BM / RP) % NW == 0 || piece < BM / RP) {
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void*)(a_src[it] + k0),
                     (__attribute__((address_space(3))) void*)&As[buf][piece * RP][0], 16, 0, 0);
             }
         }
 #pragma unroll
-        for (int it = 0; it < (BN / RP + 3) / 4; ++it) {
-            const int piece = wid + 4 * it, r = piece * RP + rl;
-            if ((BN / RP) % 4 == 0 || piece < BN / RP) {
+        for (int it = 0; it < (BN / RP + NW - 1) / NW; ++it) {
+            const int piece = wid + NW * it, r = piece * RP + rl;
+            if ((BN / RP) % NW == 0 || piece < BN / RP) {
                 const int gn = min(n0 + r, p.N - 1), q = pq ^ lds_swz<BK>(r);
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void*)(p.W + (int64_t)gn * p.K + k0 + 4 * q),
@@ -356,17 +358,17 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     auto gload = [&](int k0) {
 #pragma unroll
         for (int i = 0; i < A_IT; ++i) {
-            const int f = tid + 256 * i, row = f / Q, c = (f % Q) * 4, gm = m0 + row;
+            const int f = tid + NT * i, row = f / Q, c = (f % Q) * 4, gm = m0 + row;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((A_F4 % 256 == 0 || f < A_F4) && gm < p.M)
+            if ((A_F4 % NT == 0 || f < A_F4) && gm < p.M)
                 v = *reinterpret_cast<const f32x4*>(a_row(p, gm) + k0 + c);
             ra[i] = v;
         }
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
-            const int f = tid + 256 * i, row = f / Q, c = (f % Q) * 4, gn = n0 + row;
+            const int f = tid + NT * i, row = f / Q, c = (f % Q) * 4, gn = n0 + row;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((B_F4 % 256 == 0 || f < B_F4) && gn < p.N)
+            if ((B_F4 % NT == 0 || f < B_F4) && gn < p.N)
                 v = *reinterpret_cast<const f32x4*>(p.W + (int64_t)gn * p.K + k0 + c);
             rb[i] = v;
         }
@@ -374,14 +376,14 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
     auto sstore = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < A_IT; ++i) {
-            const int f = tid + 256 * i, r = f / Q, q = f % Q;
-            if (A_F4 % 256 == 0 || f < A_F4)
+            const int f = tid + NT * i, r = f / Q, q = f % Q;
+            if (A_F4 % NT == 0 || f < A_F4)
                 *reinterpret_cast<f32x4*>(&As[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = ra[i];
         }
 #pragma unroll
         for (int i = 0; i < B_IT; ++i) {
-            const int f = tid + 256 * i, r = f / Q, q = f % Q;
-            if (B_F4 % 256 == 0 || f < B_F4)
+            const int f = tid + NT * i, r = f / Q, q = f % Q;
+            if (B_F4 % NT == 0 || f < B_F4)
                 *reinterpret_cast<f32x4*>(&Bs[buf][r][(q ^ lds_swz<BK>(r)) * 4]) = rb[i];
         }
     };
@@ -437,14 +439,14 @@ __global__ void __launch_bounds__(256, WAVES_PER_EU) gemm_lds_kernel(GemmArgs p)
         // wave's counted wait must use its own count (with the larger count for every wave, a
         // wave issuing fewer would not wait for its own pieces of tile kt: stale LDS rows)
         constexpr int AP = BM / RP, BP = BN / RP;
-        constexpr int GA_HI = (AP + 3) / 4, GA_LO = AP / 4, GB_HI = (BP + 3) / 4, GB_LO = BP / 4;
+        constexpr int GA_HI = (AP + NW - 1) / NW, GA_LO = AP / NW, GB_HI = (BP + NW - 1) / NW, GB_LO = BP / NW;
         // the per-wave counts cover every piece exactly once: (AP % 4) waves issue GA_HI, the
         // rest GA_LO (when AP % 4 == 0 all four issue GA_HI == GA_LO); same for B
-        static_assert((AP % 4) * GA_HI + (4 - AP % 4) * GA_LO == AP, "A pieces per wave");
-        static_assert((BP % 4) * GB_HI + (4 - BP % 4) * GB_LO == BP, "B pieces per wave");
-        static_assert(AP % 4 != 0 || GA_HI == GA_LO, "A pieces: equal counts");
-        static_assert(BP % 4 != 0 || GB_HI == GB_LO, "B pieces: equal counts");
-        const bool a_hi = AP % 4 == 0 || wid < AP % 4, b_hi = BP % 4 == 0 || wid < BP % 4;
+        static_assert((AP % NW) * GA_HI + (NW - AP % NW) * GA_LO == AP, "A pieces per wave");
+        static_assert((BP % NW) * GB_HI + (NW - BP % NW) * GB_LO == BP, "B pieces per wave");
+        static_assert(AP % NW != 0 || GA_HI == GA_LO, "A pieces: equal counts");
+        static_assert(BP % NW != 0 || GB_HI == GB_LO, "B pieces: equal counts");
+        const bool a_hi = AP % NW == 0 || wid < AP % NW, b_hi = BP % NW == 0 || wid < BP % NW;
         auto wait_ring = [&]() {  // wave-uniform branches over compile-time counts
             if (a_hi) {
                 if (b_hi) wait_vmcnt<(NS - 2) * (GA_HI + GB_HI)>();

@@ -34,7 +34,7 @@ struct Variant {
     Variant{TAG "<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ">", [](const GemmArgs& a, hipStream_t s) { \
                 constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
                 const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
-                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, GL>), dim3((unsigned)tiles), dim3(256), 0, s, a); \
+                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, GL>), dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a); \
             }}
 #define RVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("regs", false, WM, WN, TM, TN, EPI, WPE, BK)
 #define GVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("glds", true, WM, WN, TM, TN, EPI, WPE, BK)
@@ -214,6 +214,23 @@ int main(int argc, char** argv) {
                   {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(4, 1, 2, 9, EPI_RESID, 4, 16),
                    GVAR(4, 1, 2, 9, EPI_RESID, 3, 16), GVAR(4, 1, 2, 9, EPI_RESID, 2, 32),
                    GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "rows") {  // 6-wave blocks: 128 x 288 (whole O-proj rows)
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(2, 3, 4, 6, EPI_QKV, 3, 16),
+                   GVAR(2, 3, 2, 6, EPI_QKV, 4, 16), GVAR(2, 3, 4, 6, EPI_QKV, 2, 16),
+                   GVAR(2, 3, 4, 3, EPI_QKV, 4, 16)}, rounds, iters);
+        run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
+                  {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), GVAR(2, 3, 4, 6, EPI_RESID, 3, 16),
+                   GVAR(2, 3, 2, 6, EPI_RESID, 4, 32), GVAR(2, 3, 4, 6, EPI_RESID, 2, 32),
+                   GVAR(2, 3, 2, 6, EPI_RESID, 4, 16)}, rounds, iters);
+        run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
+                  {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(2, 3, 4, 6, EPI_RESID, 3, 16),
+                   GVAR(2, 3, 2, 6, EPI_RESID, 4, 32), GVAR(2, 3, 4, 6, EPI_RESID, 2, 32)}, rounds, iters);
+        run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 3, 4, 4, EPI_SWIGLU, 3, 16),
+                   GVAR(2, 3, 4, 4, EPI_SWIGLU, 2, 16)}, rounds, iters);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "qkvepi") {  // what the QKV epilogue costs
