@@ -18,6 +18,7 @@
 #include "attn_research.h"
 #include "attn_pair.h"
 #include "attn_persist.h"
+#include "attn_rev.h"
 
 using namespace l3;
 
@@ -57,6 +58,12 @@ struct Variant {
                 constexpr int QW = 16 * QBW * 4;                                              \
                 dim3 grid((a.L + QW - 1) / QW, a.H / 2, a.B);                                 \
                 hipLaunchKernelGGL((attn_pair_kernel<HD, QBW, KT, MIR>), grid, dim3(512), 0, s, a); \
+            }}
+
+#define AREV(HD, KT)                                                                          \
+    Variant{"rev<" #HD ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) {                   \
+                dim3 grid((a.L + 255) / 256, a.H / 2, a.B);                                   \
+                hipLaunchKernelGGL((attn_rev_kernel<HD, KT>), grid, dim3(512), 0, s, a);        \
             }}
 
 #define AVAR2(HD, QBW, G, KT, WPE)                                                            \
@@ -211,6 +218,15 @@ static void stamps(const char* path, int warm) {
 
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
+    if (argc > 3 && std::string(argv[3]) == "rev") {  // second item's tiles in reverse order
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AREV(48, 64), APAIR(48, 4, 64, true),
+                                  AVAR(48, 4, 1, 64), AREV(48, 64)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M C3 half batch (one part of the split)", 128, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "pair") {  // two items per 8-wave workgroup
         std::vector<Variant> v = {AVAR(48, 4, 1, 64), APAIR(48, 4, 64, true), APAIR(48, 4, 64, false),
                                   AVAR(48, 4, 1, 64), APAIR(48, 4, 64, true)};

@@ -46,6 +46,7 @@ for s in "$@"; do
     attndefer) step attndefer 300 tools/attn_tune 5 10 defer ;;
     attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     attnstamps) step attnstamps 120 tools/attn_tune 3 1 stamps gpurun_out/attn_stamps.bin ;;
+    attnrev) step attnrev 300 tools/attn_tune 5 10 rev ;;
     attnpair) step attnpair 300 tools/attn_tune 5 10 pair ;;
     attnpersist) step attnpersist 300 tools/attn_tune 5 10 persist ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
