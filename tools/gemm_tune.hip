@@ -36,6 +36,13 @@ struct Variant {
                 const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
                 hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, GL>), dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a); \
             }}
+// NS-deep LDS ring (counted vmcnt, NS - 1 k-tiles in flight)
+#define GVARN(WM, WN, TM, TN, EPI, WPE, BK, NS)                                                      \
+    Variant{"ring<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ",ns" #NS ">", [](const GemmArgs& a, hipStream_t s) { \
+                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
+                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
+                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, NS>), dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a); \
+            }}
 #define RVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("regs", false, WM, WN, TM, TN, EPI, WPE, BK)
 #define GVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("glds", true, WM, WN, TM, TN, EPI, WPE, BK)
 
@@ -214,6 +221,21 @@ int main(int argc, char** argv) {
                   {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(4, 1, 2, 9, EPI_RESID, 4, 16),
                    GVAR(4, 1, 2, 9, EPI_RESID, 3, 16), GVAR(4, 1, 2, 9, EPI_RESID, 2, 32),
                    GVAR(2, 2, 4, 3, EPI_RESID, 3, 16)}, rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "ring") {  // deeper k-tile prefetch on the short-K GEMMs
+        run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
+                  {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), GVARN(2, 2, 2, 3, EPI_RESID, 3, 16, 3),
+                   GVARN(2, 2, 2, 3, EPI_RESID, 4, 16, 3), GVARN(2, 2, 2, 3, EPI_RESID, 3, 32, 3),
+                   GVARN(2, 2, 4, 3, EPI_RESID, 3, 16, 3), GVARN(2, 2, 2, 3, EPI_RESID, 4, 16, 4),
+                   GVAR(2, 2, 2, 3, EPI_RESID, 3, 32)}, rounds, iters);
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVARN(2, 2, 4, 3, EPI_QKV, 3, 16, 3),
+                   GVARN(2, 2, 4, 3, EPI_QKV, 4, 16, 3), GVARN(2, 2, 4, 3, EPI_QKV, 3, 16, 4),
+                   GVAR(2, 2, 4, 3, EPI_QKV, 4, 16)}, rounds, iters);
+        run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
+                  {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVARN(2, 2, 4, 3, EPI_RESID, 3, 16, 3),
+                   GVARN(2, 2, 4, 3, EPI_RESID, 2, 32, 3)}, rounds, iters);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "rows") {  // 6-wave blocks: 128 x 288 (whole O-proj rows)
