@@ -371,6 +371,49 @@ def test_gather_pipelined_forwards_world1(tmpdir_mod):
     ctx.set_batch_split(2)
 
 
+def test_gather_overlap_entry_points_world1(tmpdir_mod):
+    """The gather's overlap with the next forward's second batch part (L3_COMM_MODE 3) is taken
+    only by l3_forward_dev right after a gather: a host forward, a forward of another batch size
+    (workspace regrowth) and a forward after a decode step all see the gathered rows and the
+    logits of their own step, bit-identical to Llama.__call__."""
+    args = synth.stories15m(24)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    VS, L = args.vocab_size, 48
+    rng = np.random.default_rng(43)
+    ids = [rng.integers(0, VS, (B, L)).astype(np.int32) for B in (16, 16, 24)]
+    ref = llama3.Llama(path, args)
+    want = [ref(x, 0)[:, 0, :] for x in ids]
+    m = llama3.Llama(path, args)
+    ctx = m.context
+    ctx.set_batch_split(2, min_tokens=1)
+    ctx.comm_init(1, 0, l3hip.comm_unique_id())
+    ids_dev = [ctx.alloc(x.nbytes) for x in ids]
+    for d, x in zip(ids_dev, ids):
+        ctx.h2d(d, x)
+    buf = ctx.alloc(24 * VS * 4)
+    dst = [ctx.alloc(24 * VS * 4) for _ in range(3)]
+    # device forward -> gather -> host forward of the next step -> its rows
+    ctx.forward_dev(ids_dev[0], 16, L, 0, buf)
+    ctx.gather_logits(buf, dst[0], [16], root=0)
+    got1 = ctx.forward(ids[1].astype(np.int64), 0)
+    np.testing.assert_array_equal(got1, want[1])
+    np.testing.assert_array_equal(ctx.d2h(np.empty((16, VS), np.float32), dst[0]), want[0])
+    # gather -> device forward of a larger batch (the workspace grows: a synchronising path)
+    ctx.forward_dev(ids_dev[1], 16, L, 0, buf)
+    ctx.gather_logits(buf, dst[1], [16], root=0)
+    ctx.forward_dev(ids_dev[2], 24, L, 0, buf)
+    ctx.gather_logits(buf, dst[2], [24], root=0)
+    np.testing.assert_array_equal(ctx.d2h(np.empty((16, VS), np.float32), dst[1]), want[1])
+    np.testing.assert_array_equal(ctx.d2h(np.empty((24, VS), np.float32), dst[2]), want[2])
+    # gather -> forward_dev -> gather, repeated, the overlap taken every step
+    for k in range(4):
+        ctx.forward_dev(ids_dev[k % 2], 16, L, 0, buf)
+        ctx.gather_logits(buf, dst[k % 2], [16], root=0)
+    for k in range(2):
+        np.testing.assert_array_equal(ctx.d2h(np.empty((16, VS), np.float32), dst[k]), want[k])
+    ctx.set_batch_split(2)
+
+
 # ---- decode state / graph replay ------------------------------------------------------------
 
 @pytest.mark.parametrize("case", ["all_equal", "pair_tie_zero_rest", "nan_rows"])
