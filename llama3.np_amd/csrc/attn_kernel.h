@@ -76,17 +76,21 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     const int key_end = start_pos + q_hi;  // keys [0, key_end) are needed
     const int ntiles = (key_end + KT - 1) / KT;
 
+    // Loads are unpredicated, from clamped (in-bounds) rows: a query lane past L computes on a
+    // copy of row L - 1 and is never stored (each lane's softmax state is its own query's), and
+    // a key past Smax is past key_end, so every valid query masks it.  Predicated loads compiled
+    // to exec-masked branches whose register copies waited for every load in flight (an
+    // s_waitcnt vmcnt(0) after the second q load of the prologue).
     f32x4 qreg[QBW][ND];
     f32x4 o[QBW][ND];
     float m_run[QBW], l_run[QBW];
 #pragma unroll
     for (int j = 0; j < QBW; ++j) {
-        const int ql = q_lo + qblk[j] * 16 + fq;
+        const int ql = min(q_lo + qblk[j] * 16 + fq, p.L - 1);
         const float* src = p.q + ((int64_t)b * p.L + ql) * qdim + h * HD + fk;
 #pragma unroll
         for (int dg = 0; dg < ND; ++dg) {
-            qreg[j][dg] = (ql < p.L) ? *reinterpret_cast<const f32x4*>(src + dg * 16)
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+            qreg[j][dg] = *reinterpret_cast<const f32x4*>(src + dg * 16);
             o[j][dg] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
         m_run[j] = -INFINITY;
@@ -100,14 +104,11 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
         for (int i = 0; i < K_IT; ++i) {
             const int f = tid + 256 * i;
             const int row = f / (HD / 4), c = (f % (HD / 4)) * 4;
-            const int key = tile * KT + row;
-            f32x4 vk = {0.f, 0.f, 0.f, 0.f}, vv = vk;
-            if ((K_F4 % 256 == 0 || f < K_F4) && key < p.Smax) {
-                vk = *reinterpret_cast<const f32x4*>(p.cache_k + (kv_base + key) * HD + c);
-                vv = *reinterpret_cast<const f32x4*>(p.cache_v + (kv_base + key) * HD + c);
+            const int key = min(tile * KT + row, p.Smax - 1);
+            if (K_F4 % 256 == 0 || f < K_F4) {
+                rk[i] = *reinterpret_cast<const f32x4*>(p.cache_k + (kv_base + key) * HD + c);
+                rv[i] = *reinterpret_cast<const f32x4*>(p.cache_v + (kv_base + key) * HD + c);
             }
-            rk[i] = vk;
-            rv[i] = vv;
         }
     };
     auto sstore = [&](int buf) {
@@ -262,19 +263,18 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
     const f32x4* K4 = reinterpret_cast<const f32x4*>(p.cache_k + kv_base);
     const f32x4* V4 = reinterpret_cast<const f32x4*>(p.cache_v + kv_base);
     const int rg = tid / D4, d4 = tid - rg * D4;
+    // the entry loads are unpredicated, from clamped (in-bounds) rows — a V row past S or an
+    // O-proj row past D is loaded but never used; predicated loads compiled to exec-masked
+    // branches whose register copies waited for every load in flight (one round trip more)
     f32x4 vpre[VP];
 #pragma unroll
-    for (int t = 0; t < VP; ++t) {
-        const int k = rg + t * R;
-        vpre[t] = (rg < R && k < S) ? V4[(int64_t)k * D4 + d4] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int t = 0; t < VP; ++t) vpre[t] = V4[(int64_t)min(rg + t * R, S - 1) * D4 + d4];
     const int orow = blockIdx.z * 64 + (tid >> 2), opart = tid & 3;
     f32x4 wpre[FUSE_O ? WQ : 1];
     if constexpr (FUSE_O) {
-        const bool ok = orow < p.D;
-        const f32x4* w4 = reinterpret_cast<const f32x4*>(p.wo + (int64_t)(ok ? orow : 0) * (p.H * HD) + h * HD) + opart * WQ;
+        const f32x4* w4 = reinterpret_cast<const f32x4*>(p.wo + (int64_t)min(orow, p.D - 1) * (p.H * HD) + h * HD) + opart * WQ;
 #pragma unroll
-        for (int i = 0; i < WQ; ++i) wpre[i] = ok ? w4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < WQ; ++i) wpre[i] = w4[i];
     }
     const f32x4* q4 = reinterpret_cast<const f32x4*>(p.q + ((int64_t)b * p.H + h) * HD);
     f32x4 q[D4];
@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
 #pragma unroll
         for (int t = 0; t < VP; ++t) {
             const int k = rg + t * R;
-            if (k < S) acc += sc[k] * vpre[t];
+            acc += (k < S ? sc[min(k, S - 1)] : 0.f) * vpre[t];
         }
         for (int k = rg + VP * R; k < S; k += R) acc += sc[k] * V4[(int64_t)k * D4 + d4];
         reinterpret_cast<f32x4*>(red)[rg * D4 + d4] = acc;

@@ -212,16 +212,27 @@ __global__ void __launch_bounds__(256) splitk_finish_kernel(GemmArgs p) {
     const int row = (int)(idx / nc), c4 = (int)(idx - (int64_t)row * nc);
     const int S = p.splits;
     const int64_t MN = (int64_t)p.M * p.N;
+    // every slice's load is issued before the first add (unpredicated, clamped slice index;
+    // slices past S add zero): a loop of dependent loads cost one round trip per slice
+    constexpr int SMAX = 16;  // launch_split_cfg: S <= 16
     float rs = 1.0f;
     if (p.norm) {
+        float t[SMAX];
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) t[k] = p.ws[S * MN + (int64_t)min(k, S - 1) * p.M + row];
         float v = 0.f;
-        for (int k = 0; k < S; ++k) v += p.ws[S * MN + (int64_t)k * p.M + row];
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) v += k < S ? t[k] : 0.f;
         rs = __builtin_amdgcn_rsqf(v * (1.0f / (float)p.K) + p.eps);
     }
     auto sum_at = [&](int col) {
         const float* src = p.ws + (int64_t)row * p.N + col;
-        f32x4 v = *reinterpret_cast<const f32x4*>(src);
-        for (int k = 1; k < S; ++k) v += *reinterpret_cast<const f32x4*>(src + k * MN);
+        f32x4 t[SMAX];
+#pragma unroll
+        for (int k = 0; k < SMAX; ++k) t[k] = *reinterpret_cast<const f32x4*>(src + (int64_t)min(k, S - 1) * MN);
+        f32x4 v = t[0];
+#pragma unroll
+        for (int k = 1; k < SMAX; ++k) v += k < S ? t[k] : f32x4{0.f, 0.f, 0.f, 0.f};
         return v;
     };
     if constexpr (EPI == EPI_SWIGLU) {
@@ -683,16 +694,26 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     f32x4 xv[DIRECT ? CH : 1];
     f32x4 xp[XPARTS ? CH : 1][XPARTS ? GEMV_MAXP : 1];
     const f32x4* P4 = reinterpret_cast<const f32x4*>(p.parts) + (int64_t)m0 * p.nparts * K4;
+    // Row-blocked forms (MR > 1): W loads unpredicated from clamped addresses, x zeroed past K
+    // where it is used (their predicated loads compiled to exec-masked branches that each waited
+    // for the load before issuing the next).  The one-row form keeps predicated loads: there
+    // hipcc already issued them all before the first wait, and the unpredicated form let it
+    // interleave loads and waits instead.
     auto load_chunk = [&](int t0) {
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
-            const int k4 = j + LPU * (t0 + t);
+            const int k4 = j + LPU * (t0 + t), kk = min(k4, K4 - 1);
 #pragma unroll
-            for (int r = 0; r < ROWS; ++r)
-                w[r][t] = k4 >= K4 ? f32x4{0.f, 0.f, 0.f, 0.f}
-                          : NT ? __builtin_nontemporal_load(&W4[(int64_t)wrow[r] * K4 + k4])
-                               : W4[(int64_t)wrow[r] * K4 + k4];
-            if constexpr (DIRECT) xv[t] = X4[min(k4, K4 - 1)];
+            for (int r = 0; r < ROWS; ++r) {
+                if constexpr (DIRECT)
+                    w[r][t] = k4 >= K4 ? f32x4{0.f, 0.f, 0.f, 0.f}
+                              : NT ? __builtin_nontemporal_load(&W4[(int64_t)wrow[r] * K4 + k4])
+                                   : W4[(int64_t)wrow[r] * K4 + k4];
+                else
+                    w[r][t] = NT ? __builtin_nontemporal_load(&W4[(int64_t)wrow[r] * K4 + kk])
+                                 : W4[(int64_t)wrow[r] * K4 + kk];
+            }
+            if constexpr (DIRECT) xv[t] = X4[kk];
             if constexpr (XPARTS) {
 #pragma unroll
                 for (int pp = 0; pp < GEMV_MAXP; ++pp)
@@ -759,6 +780,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     }
     // stage the row block (rows past Mb zero: branch-free FMA loop), SU loads in flight per
     // thread before the first LDS store (a serial load -> store walk costs a round trip each)
+    // (unpredicated loads from clamped addresses, zeroed after they land: predicated loads
+    // compiled to exec-masked branches that waited for each load before issuing the next)
     constexpr int SU = 8;
     if constexpr (!DIRECT) {
         for (int f0 = tid; f0 < MR * K4; f0 += 256 * SU) {
@@ -766,12 +789,14 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
 #pragma unroll
             for (int u = 0; u < SU; ++u) {
                 const int f = f0 + 256 * u, m = f / K4, k4 = f - m * K4;
-                v[u] = (f < MR * K4 && m < Mb) ? reinterpret_cast<const f32x4*>(a_row(p, m0 + m))[k4]
-                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+                const bool ok = f < MR * K4 && m < Mb;
+                v[u] = reinterpret_cast<const f32x4*>(a_row(p, m0 + (ok ? m : 0)))[ok ? k4 : 0];
             }
 #pragma unroll
-            for (int u = 0; u < SU; ++u)
-                if (f0 + 256 * u < MR * K4) reinterpret_cast<f32x4*>(xs)[f0 + 256 * u] = v[u];
+            for (int u = 0; u < SU; ++u) {
+                const int f = f0 + 256 * u, m = f / K4;
+                if (f < MR * K4) reinterpret_cast<f32x4*>(xs)[f] = m < Mb ? v[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
         }
         __syncthreads();
     }
@@ -799,7 +824,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
 #pragma unroll
         for (int t = 0; t < CH; ++t) {
             if (t0 + t >= nt) break;  // wave-uniform
-            // lanes past K read a clamped (finite) x against their zero W and count no norm
+            // lanes past K: the one-row form reads a clamped (finite) x against its zero W and
+            // counts no norm; the row-blocked form holds clamped W and zeroes x
             const int k4 = j + LPU * (t0 + t), kk = min(k4, K4 - 1);
             const float in = k4 < K4 ? 1.f : 0.f;
             f32x4 x[MR];
@@ -807,7 +833,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                 x[0] = xv[t];
             } else {
 #pragma unroll
-                for (int m = 0; m < MR; ++m) x[m] = reinterpret_cast<const f32x4*>(xs + m * p.K)[kk];
+                for (int m = 0; m < MR; ++m)
+                    x[m] = k4 < K4 ? reinterpret_cast<const f32x4*>(xs + m * p.K)[kk] : f32x4{0.f, 0.f, 0.f, 0.f};
             }
 #pragma unroll
             for (int m = 0; m < MR; ++m) {

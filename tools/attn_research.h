@@ -20,7 +20,8 @@ __device__ unsigned long long* g_attn_stamps;
 // structure), 2 p = s (no exp), 4 no K/V loads after tile 0, 8 no barrier in the tile loop,
 // 16 no softmax bookkeeping (no max / rescale / sum); 32 (timing study, results correct): K/V
 // tiles prefetched two ahead through two register sets; 64 / 128 / 256 (timing study, results
-// correct): s_setprio(1) around both MFMA clusters / the score cluster / the P.V cluster
+// correct): s_setprio(1) around both MFMA clusters / the score cluster / the P.V cluster;
+// 1024 (timing study, results correct): K/V tile 0 before q, raw prologue barrier
 //
 // DEFER (HD 48): three K/V slots instead of two, and the diagonal (masked) units of the even
 // q-block slots j (C3: the even tiles' diagonal units) run one barrier interval later, first
@@ -89,23 +90,6 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
     const int key_end = start_pos + q_hi;  // keys [0, key_end) are needed
     const int ntiles = (key_end + KT - 1) / KT;
 
-    f32x4 qreg[QBW][ND];
-    f32x4 o[QBW][ND];
-    float m_run[QBW], l_run[QBW];
-#pragma unroll
-    for (int j = 0; j < QBW; ++j) {
-        const int ql = q_lo + qblk[j] * 16 + fq;
-        const float* src = p.q + ((int64_t)b * p.L + ql) * qdim + h * HD + fk;
-#pragma unroll
-        for (int dg = 0; dg < ND; ++dg) {
-            qreg[j][dg] = (ql < p.L) ? *reinterpret_cast<const f32x4*>(src + dg * 16)
-                                     : f32x4{0.f, 0.f, 0.f, 0.f};
-            o[j][dg] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        m_run[j] = -INFINITY;
-        l_run[j] = 0.f;
-    }
-
     const int64_t kv_base = ((int64_t)b * p.KVH + kvh) * p.Smax;
     f32x4 rk[K_IT], rv[K_IT];
     f32x4 rk2[(ABL & 32) ? K_IT : 1], rv2[(ABL & 32) ? K_IT : 1];
@@ -138,13 +122,38 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
     };
     auto gload = [&](int tile) { gload_into(tile, rk, rv); };
     auto sstore = [&](int buf) { sstore_from(buf, rk, rv); };
+    // ABL & 1024 (timing study, results correct): K/V tile 0 is fetched before q, and the
+    // prologue barrier waits only for its LDS stores, so the q loads land during tile 0
+    if constexpr ((ABL & 1024) != 0) gload(0);
+    f32x4 qreg[QBW][ND];
+    f32x4 o[QBW][ND];
+    float m_run[QBW], l_run[QBW];
+#pragma unroll
+    for (int j = 0; j < QBW; ++j) {
+        const int ql = q_lo + qblk[j] * 16 + fq;
+        const float* src = p.q + ((int64_t)b * p.L + ql) * qdim + h * HD + fk;
+#pragma unroll
+        for (int dg = 0; dg < ND; ++dg) {
+            qreg[j][dg] = (ql < p.L) ? *reinterpret_cast<const f32x4*>(src + dg * 16)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+            o[j][dg] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        m_run[j] = -INFINITY;
+        l_run[j] = 0.f;
+    }
 
-    gload(0);
+
+    if constexpr ((ABL & 1024) == 0) gload(0);
     sstore(0);
     if constexpr ((ABL & 32) != 0) {
         if (ntiles > 1) gload(1);  // set A holds tile 1
     }
-    __syncthreads();
+    if constexpr ((ABL & 1024) != 0) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    } else {
+        __syncthreads();
+    }
     stamp(1);
     int cur = 0;  // slot of this tile (tile % NS)
     for (int tile = 0; tile < ntiles; ++tile) {

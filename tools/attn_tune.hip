@@ -218,6 +218,14 @@ static void stamps(const char* path, int warm) {
 
 int main(int argc, char** argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 5, iters = argc > 2 ? atoi(argv[2]) : 10;
+    if (argc > 3 && std::string(argv[3]) == "early") {  // K/V tile 0 before q, raw prologue barrier
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AABL(0), AABL(1024), AVAR(48, 4, 1, 64), AABL(1024)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M C3 half batch (one part of the split)", 128, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "rev") {  // second item's tiles in reverse order
         std::vector<Variant> v = {AVAR(48, 4, 1, 64), AREV(48, 64), APAIR(48, 4, 64, true),
                                   AVAR(48, 4, 1, 64), AREV(48, 64)};

@@ -47,6 +47,7 @@ for s in "$@"; do
     attndefer) step attndefer 300 tools/attn_tune 5 10 defer ;;
     attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     attnstamps) step attnstamps 120 tools/attn_tune 3 1 stamps gpurun_out/attn_stamps.bin ;;
+    attnearly) step attnearly 300 tools/attn_tune 5 10 early ;;
     attnrev) step attnrev 300 tools/attn_tune 5 10 rev ;;
     attnpair) step attnpair 300 tools/attn_tune 5 10 pair ;;
     attnpersist) step attnpersist 300 tools/attn_tune 5 10 persist ;;
