@@ -159,6 +159,16 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
                 *reinterpret_cast<f32x4*>(p.C + (int64_t)row * p.ldc + hcol) = v;
             }
         } else {
+            // EPI_RESID without the prefetch: the row's TN residual float4s are loaded together
+            // (unpredicated, clamped column) before the first add — a predicated load per tile
+            // compiled to a branch that waited for it before the next was issued
+            f32x4 rrow[(EPI == EPI_RESID && !RES_PREFETCH) ? TN : 1];
+            if constexpr (EPI == EPI_RESID && !RES_PREFETCH) {
+                const float* rb = res_row(p, row);
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    rrow[j] = *reinterpret_cast<const f32x4*>(rb + min(ncol0 + j * 16 + fq4, p.N - 4));
+            }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int col = ncol0 + j * 16 + fq4;
@@ -167,7 +177,7 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
                 float* dst = p.C + (int64_t)row * p.ldc + col;
                 if constexpr (EPI == EPI_RESID) {
                     if constexpr (RES_PREFETCH) v += res[i * TN + j];
-                    else v += *reinterpret_cast<const f32x4*>(res_at(p, row, col));
+                    else v += rrow[j];
                 } else {
                     v *= sc;
                 }
@@ -480,15 +490,14 @@ __global__ void __launch_bounds__(64 * WM * WN, WAVES_PER_EU) gemm_lds_kernel(Ge
             if (kt + NS - 1 < nk) glds_tile((kt + NS - 1) % NS, kb + (kt + NS - 1) * BK);
             if constexpr (RES_PREFETCH) {
                 if (kt == nk - 1) {
+                    const float* rb[TM];
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) rb[i] = res_row(p, min(m0 + arow0 + i * 16 + frow, p.M - 1));
 #pragma unroll
                     for (int i = 0; i < TM; ++i)
 #pragma unroll
-                        for (int j = 0; j < TN; ++j) {
-                            const int row = m0 + arow0 + i * 16 + frow, col = n0 + brow0 + j * 16 + fk;
-                            res[i * TN + j] = (row < p.M && col < p.N)
-                                                  ? *reinterpret_cast<const f32x4*>(res_at(p, row, col))
-                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
-                        }
+                        for (int j = 0; j < TN; ++j)
+                            res[i * TN + j] = *reinterpret_cast<const f32x4*>(rb[i] + min(n0 + brow0 + j * 16 + fk, p.N - 4));
                 }
             }
             compute(kt % NS);
@@ -516,16 +525,18 @@ __global__ void __launch_bounds__(64 * WM * WN, WAVES_PER_EU) gemm_lds_kernel(Ge
     }
     // last k-tile, peeled: the residual loads are issued first so their latency hides behind
     // this tile's MFMAs
+    // (unpredicated, from clamped rows / columns — rows and columns past the edge are never
+    // stored — so all TM x TN loads are in flight together: predicated ones compiled to
+    // branches that waited for each load before issuing the next)
     if constexpr (RES_PREFETCH) {
+        const float* rb[TM];  // a gathered embedding row's index is read once per row
+#pragma unroll
+        for (int i = 0; i < TM; ++i) rb[i] = res_row(p, min(m0 + arow0 + i * 16 + frow, p.M - 1));
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int row = m0 + arow0 + i * 16 + frow, col = n0 + brow0 + j * 16 + fk;
-                res[i * TN + j] = (row < p.M && col < p.N)
-                                      ? *reinterpret_cast<const f32x4*>(res_at(p, row, col))
-                                      : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+            for (int j = 0; j < TN; ++j)
+                res[i * TN + j] = *reinterpret_cast<const f32x4*>(rb[i] + min(n0 + brow0 + j * 16 + fk, p.N - 4));
     }
     compute((nk - 1) & 1);
     }

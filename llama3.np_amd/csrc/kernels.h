@@ -195,9 +195,12 @@ __device__ __forceinline__ const float* a_row(const GemmArgs& p, int64_t r) {
     return p.A + (p.a_rows ? (int64_t)p.a_rows[r] : r) * p.lda;
 }
 // residual operand of EPI_RESID at (row, col): C itself, or the gathered embedding row
+__device__ __forceinline__ const float* res_row(const GemmArgs& p, int64_t row) {
+    return p.res_src ? p.res_src + (p.res_rows ? (int64_t)p.res_rows[row] : row) * p.ldc
+                     : p.C + row * p.ldc;
+}
 __device__ __forceinline__ const float* res_at(const GemmArgs& p, int64_t row, int col) {
-    return p.res_src ? p.res_src + (p.res_rows ? (int64_t)p.res_rows[row] : row) * p.ldc + col
-                     : p.C + row * p.ldc + col;
+    return res_row(p, row) + col;
 }
 
 struct AttnArgs {
