@@ -691,6 +691,33 @@ def test_cache_edges_full_context_single_token_prompt(tmpdir_mod):
         _close(got, want)
 
 
+@pytest.mark.parametrize("dim,heads,kv_heads,max_seq", [(64, 4, 2, 100), (96, 2, 2, 77)])
+def test_ragged_cache_end_against_oracle(tmpdir_mod, dim, heads, kv_heads, max_seq):
+    """A max_seq_len that is no multiple of the attention's 64-key tile and prompts whose
+    lengths are no multiple of its 16-query blocks: the last K/V tile runs past the cache end
+    (its rows are read from clamped addresses and masked) and the last q-block past L (its lanes
+    are computed on a copy of row L - 1 and never stored).  Prefill, a chunk ending 10 short
+    of max_seq_len, then decode steps to the last slot, all against the live oracle."""
+    from config import ModelArgs
+    args = ModelArgs(dim=dim, n_layers=2, n_heads=heads, n_kv_heads=kv_heads, vocab_size=512,
+                     max_seq_len=max_seq, max_batch_size=3)
+    hidden = 2 * dim + 64
+    w, path = _model(tmpdir_mod, args, hidden, 17 + dim, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(53)
+    B, M = args.max_batch_size, args.max_seq_len
+    p0 = rng.integers(0, args.vocab_size, (B, 37))
+    _close(m(p0, 0), ref(p0, 0))
+    chunk = rng.integers(0, args.vocab_size, (B, M - 10 - 37))
+    got, want = m(chunk, 37), ref(chunk, 37)
+    _close(got, want)
+    for pos in range(M - 10, M):
+        nxt = want[:, -1, :].argmax(-1)[:, None]
+        got, want = m(nxt, pos), ref(nxt, pos)
+        _close(got, want)
+
+
 @pytest.fixture(scope="module")
 def c5_weights():
     """The c5_slice golden's 2-layer Llama-3-8B-shaped weights (6 GB, regenerated from the

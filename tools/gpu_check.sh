@@ -94,6 +94,7 @@ for s in "$@"; do
     spawn1) step spawn1 300 python bench.py --spawn --rccl --steps 20 --warmup 3 --no-cpu-baseline ;;
     c5deep) step c5deep 900 python -u -m pytest tests/test_gpu_parity.py -k c5_full_depth -x -v -s --timeout 900 --timeout-method thread ;;
     testsv) step tests 1200 python -u -m pytest tests -m gpu -v -rfP --timeout 900 --timeout-method thread ;;
+    ragged) step ragged 300 python -u -m pytest tests/test_gpu_parity.py -k "ragged or cache_edges or head_dims or chunk" -x -q --timeout 300 --timeout-method thread ;;
     gath3) L3_COMM_MODE=3 step gath3 300 python -u -m pytest tests/test_gpu_parity.py -k gather -x -q --timeout 300 --timeout-method thread ;;
     race3) L3_COMM_MODE=3 step race3 300 python tools/gather_race_check.py 10 ;;
     benchr3) L3_COMM_MODE=3 step benchr3 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
