@@ -68,13 +68,13 @@ static hipError_t launch_split(int epi, const GemmArgs& a, hipStream_t s) {
     }
 }
 
-template <int EPI, int MR, int LPU, bool PARTS = false, bool NT = false>
+template <int EPI, int MR, int LPU, bool PARTS = false, bool NT = false, bool FOLD = false>
 static hipError_t launch_gemv_lpu(const GemmArgs& a, hipStream_t s) {
     const int units = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? a.N / 2 : a.N;
     const int per_block = 4 * (64 / LPU);
     const dim3 grid((unsigned)((units + per_block - 1) / per_block), (unsigned)((a.M + MR - 1) / MR)),
         block(256);
-    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU, PARTS, NT>), grid, block, MR == 1 ? 0 : (size_t)MR * a.K * 4, s, a);
+    hipLaunchKernelGGL((gemv_kernel<EPI, MR, LPU, PARTS, NT, FOLD>), grid, block, MR == 1 ? 0 : (size_t)MR * a.K * 4, s, a);
     return hipGetLastError();
 }
 
@@ -198,6 +198,17 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         }
     }
     if (a.amax_part && (epi != EPI_STORE || !gemv_store_blocks(a))) return hipErrorInvalidValue;
+    if (a.pos_adv && !a.amax_part) return hipErrorInvalidValue;
+    if (a.amax_in) {  // layer-0 QKV of a captured batch-1 decode step with the previous argmax folded in
+        if (epi != EPI_QKV || a.M != 1 || !gemv_direct(a) || a.col_base || a.a_rows || a.amax_in_n < 1 ||
+            !a.amax_ids || !a.amax_st)
+            return hipErrorInvalidValue;
+        switch (gemv_lpu(a)) {
+            case 16: return launch_gemv_lpu<EPI_QKV, 1, 16, false, false, true>(a, s);
+            case 32: return launch_gemv_lpu<EPI_QKV, 1, 32, false, false, true>(a, s);
+            default: return launch_gemv_lpu<EPI_QKV, 1, 64, false, false, true>(a, s);
+        }
+    }
     if (a.force_skinny || (gemm_is_gemv(a) && use_skinny(a))) {
         switch (epi) {
             case EPI_SWIGLU: return launch_skinny<EPI_SWIGLU, 2>(a, s);

@@ -668,10 +668,17 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs p) {
 // once per call and that do not fit the caches anyway (Llama-3-shape decode: 67 MB - 2.1 GB per
 // launch); the small layer weights of stories15M stay on the default policy (they are re-read
 // from the caches every step).
-template <int EPI, int MR, int LPU, bool PARTS = false, bool NT = false>
+//
+// FOLD (EPI_QKV, MR = 1: layer 0 of a captured batch-1 decode step that follows another in the
+// same graph): the previous step's greedy argmax (llama3.py:320) happens here instead of in a
+// launch of its own — every block reduces that step's lm_head partials (GemmArgs::amax_in, a few
+// KB from L2, loaded beside the W pieces) to the id whose embedding row is this step's input
+// (:287); block 0 publishes the id (amax_ids, amax_st's history).
+template <int EPI, int MR, int LPU, bool PARTS = false, bool NT = false, bool FOLD = false>
 __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     extern __shared__ __attribute__((aligned(16))) float xs[];  // [MR][K]
     static_assert(!PARTS || MR == 1, "partial rows only on the one-row GEMV");
+    static_assert(!FOLD || (MR == 1 && EPI == EPI_QKV && !PARTS), "the folded argmax feeds a one-row QKV");
     constexpr int ROWS = (EPI == EPI_SWIGLU || EPI == EPI_QKV) ? 2 : 1;
     constexpr int UPW = 64 / LPU;  // units per wave
     constexpr int CH = PARTS ? 4 : 8;  // float4 per W row per lane in flight
@@ -700,7 +707,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     // pieces — one memory round trip, no LDS staging pass and no block barrier; MR > 1 stages
     // the rows once in LDS (re-read by every unit of the block)
     constexpr bool DIRECT = MR == 1;
-    const f32x4* X4 = reinterpret_cast<const f32x4*>(a_row(p, m0));
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(FOLD ? p.A : a_row(p, m0));
     f32x4 w[ROWS][CH];
     f32x4 xv[DIRECT ? CH : 1];
     f32x4 xp[XPARTS ? CH : 1][XPARTS ? GEMV_MAXP : 1];
@@ -724,7 +731,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                     w[r][t] = NT ? __builtin_nontemporal_load(&W4[(int64_t)wrow[r] * K4 + kk])
                                  : W4[(int64_t)wrow[r] * K4 + kk];
             }
-            if constexpr (DIRECT) xv[t] = X4[kk];
+            if constexpr (DIRECT) {
+                if (!FOLD || t0) xv[t] = X4[kk];  // FOLD: chunk 0's x once the id is known
+            }
             if constexpr (XPARTS) {
 #pragma unroll
                 for (int pp = 0; pp < GEMV_MAXP; ++pp)
@@ -741,6 +750,23 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                 for (int pp = 0; pp < GEMV_MAXP; ++pp) xv[t] += xp[t][pp];
         }
     };
+    // FOLD: the previous step's partials, loaded before the W pieces so the reduction waits for
+    // them alone (clamped indices: a repeated partial does not change an argmax)
+    constexpr int FU = 8;
+    ArgmaxPart fq[FOLD ? FU : 1];
+    int f_pos = 0, f_base = 0, f_cap = 0;  // block 0: the history fields, fetched up front
+    int32_t* f_hist = nullptr;
+    if constexpr (FOLD) {
+#pragma unroll
+        for (int u = 0; u < FU; ++u) fq[u] = p.amax_in[min(u * 256 + tid, p.amax_in_n - 1)];
+        if (blockIdx.x == 0) {
+            const DecState* st = p.amax_st;
+            f_pos = st->pos;
+            f_base = st->hist_base;
+            f_cap = st->hist_cap;
+            f_hist = st->hist;
+        }
+    }
     load_chunk(0);  // in flight while the input rows are staged
     // the epilogue's own operands (EPI_RESID: the residual; EPI_QKV: the RoPE cos / sin of the
     // pair) do not depend on the dot products: fetch them now, not after the reduction (one
@@ -787,6 +813,43 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                     (qkv_sec == 1 ? p.cache_k : p.cache_v) +
                     (((int64_t)bidx * p.KVH + qkv_head) * p.Smax + pos) * p.HD + qkv_d);
             }
+        }
+    }
+    if constexpr (FOLD) {
+        float bv = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int base = 0;; base += FU * 256) {
+#pragma unroll
+            for (int u = 0; u < FU; ++u)
+                if (argmax_better(fq[u].v, fq[u].i, bv, bi)) { bv = fq[u].v; bi = fq[u].i; }
+            if (base + FU * 256 >= p.amax_in_n) break;
+#pragma unroll
+            for (int u = 0; u < FU; ++u) fq[u] = p.amax_in[min(base + FU * 256 + u * 256 + tid, p.amax_in_n - 1)];
+        }
+        group_argmax<64>(bv, bi, lane);
+        __shared__ float fv[4];
+        __shared__ int fi[4];
+        if (lane == 0) {
+            fv[wid] = bv;
+            fi[wid] = bi;
+        }
+        __syncthreads();
+        bv = fv[0];
+        bi = fi[0];
+#pragma unroll
+        for (int w2 = 1; w2 < 4; ++w2)
+            if (argmax_better(fv[w2], fi[w2], bv, bi)) {
+                bv = fv[w2];
+                bi = fi[w2];
+            }
+        X4 = reinterpret_cast<const f32x4*>(p.A + (int64_t)bi * p.lda);
+#pragma unroll
+        for (int t = 0; t < CH; ++t) xv[t] = X4[min(j + LPU * t, K4 - 1)];
+        if (blockIdx.x == 0 && tid == 0) {
+            p.amax_ids[0] = bi;
+            // the previous step's position: its lm_head already moved pos on (pos_adv)
+            const int q = f_pos - 1 - f_base;
+            if (f_hist && q >= 0 && q < f_cap) f_hist[q] = bi;
         }
     }
     // stage the row block (rows past Mb zero: branch-free FMA loop), SU loads in flight per
@@ -885,6 +948,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
                         bi = si[w2];
                     }
                 p.amax_part[blockIdx.x] = ArgmaxPart{bv, bi};
+                if (p.pos_adv && blockIdx.x == 0) p.pos_adv->pos += 1;
             }
         }
     }

@@ -32,6 +32,16 @@ struct ArgmaxPart {
     int i;
 };
 
+// Device-resident state of the greedy decode loop (graph replay).  pos is first, so &st->pos
+// is the pos_dev the captured kernels read.
+struct DecState {
+    int pos;           // start_pos of the next decode step; the argmax advances it
+    int hist_base;     // generate loop: the ids of the step at position q go to
+    int hist_cap;      //   hist[(q - hist_base) * B + b] while 0 <= q - hist_base < hist_cap
+    unsigned arrive;   // argmax_kernel's block arrival count (0 between launches)
+    int32_t* hist;     // null: no history
+};
+
 struct GemmArgs {
     const float* A; int64_t lda;   // A rows, row stride (floats)
     const float* W;                // [N, K] row-major
@@ -69,6 +79,15 @@ struct GemmArgs {
     // EPI_STORE on the one-row GEMV (batch-1 lm_head): also the block's (value, index) argmax
     // over its columns -> amax_part[blockIdx.x], reduced by launch_argmax_parts
     ArgmaxPart* amax_part;
+    DecState* pos_adv;             // ... and block 0 moves the decode position on (a captured step
+                                   // whose argmax the next step's layer-0 QKV folds in)
+    // EPI_QKV on the one-row GEMV (a captured batch-1 decode step after the first of a graph): the
+    // A row is the embedding row of the previous step's greedy id, reduced by every block from
+    // that step's lm_head partials (amax_in, amax_in_n); block 0 also stores the id to amax_ids[0]
+    // (the layer-0 gate|up's embedding row) and to the generate history of amax_st at pos - 1
+    const ArgmaxPart* amax_in; int amax_in_n;
+    int32_t* amax_ids;
+    DecState* amax_st;
     // Split-K (short M against a long K, gemm.hip launch_split): the caller's workspace of ws_cap
     // floats (null: no split); the k-slices leave raw partial tiles [splits][M][N] and partial
     // row sums of squares [splits][M] there, and splitk_finish_kernel applies the epilogue
@@ -81,15 +100,6 @@ struct GemmArgs {
 constexpr int GEMV_MAXP = 8;
 constexpr int KV_BAK_SLOTS = 32;  // > the decode steps ever run ahead (runtime.hip SPEC_AHEAD)
 
-// Device-resident state of the greedy decode loop (graph replay).  pos is first, so &st->pos
-// is the pos_dev the captured kernels read.
-struct DecState {
-    int pos;           // start_pos of the next decode step; the argmax advances it
-    int hist_base;     // generate loop: the ids of the step at position q go to
-    int hist_cap;      //   hist[(q - hist_base) * B + b] while 0 <= q - hist_base < hist_cap
-    unsigned arrive;   // argmax_kernel's block arrival count (0 between launches)
-    int32_t* hist;     // null: no history
-};
 
 // Exchange with lane ^ 16 and lane ^ 32 through v_permlane16_swap / v_permlane32_swap (VALU)
 // rather than ds_bpermute: a bpermute is an LDS-pipe round trip whose lgkmcnt wait also
@@ -233,7 +243,7 @@ hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out,
                          DecState* st = nullptr);
 // the same result from the lm_head's per-block partials (one row: GemmArgs::amax_part)
 hipError_t launch_argmax_parts(const ArgmaxPart* parts, int nparts, int32_t* out, hipStream_t s,
-                               DecState* st = nullptr);
+                               DecState* st = nullptr, int hist_off = 0);
 // blocks of the one-row lm_head GEMV (= its partial count when amax_part is set), 0 otherwise
 int gemv_store_blocks(const GemmArgs& a);
 // true when launch_gemm runs this shape on the row-blocked GEMV (short M)

@@ -26,8 +26,10 @@ __device__ __forceinline__ float wave_max(float v) {
 // block-wide finish of a row argmax (1024 threads, every thread's candidate in best / bi): the
 // id to out[blockIdx.x]; in a captured decode step also the generate history and the position
 // advance (last-arriving row)
+// hist_off 1: the step's lm_head has already moved the position on (GemmArgs::pos_adv), so the
+// id belongs at pos - 1 and the position stays
 __device__ __forceinline__ void argmax_finish(float best, int bi, int32_t* __restrict__ out,
-                                              DecState* __restrict__ st) {
+                                              DecState* __restrict__ st, int hist_off = 0) {
     constexpr int NT = 1024;
     const int tid = threadIdx.x;
     group_argmax<64>(best, bi, tid & 63);
@@ -46,9 +48,11 @@ __device__ __forceinline__ void argmax_finish(float best, int bi, int32_t* __res
                 // to arrive moves the loop one position on (llama3.py:312-318).  Every block
                 // reads pos before its arrival (the fence orders the read and the history store
                 // before the atomic), so none sees the advanced value.
-                const int pos = st->pos, q = pos - st->hist_base;
+                const int pos = st->pos - hist_off, q = pos - st->hist_base;
                 if (st->hist && q >= 0 && q < st->hist_cap) st->hist[(int64_t)q * gridDim.x + blockIdx.x] = bi;
-                if (gridDim.x == 1) {
+                if (hist_off) {
+                    // the lm_head of this step already moved the position on
+                } else if (gridDim.x == 1) {
                     // one row (batch-1 decode): this thread is the only reader of pos in this
                     // launch, so it advances it directly — no agent-scope fence (≈1-3 µs of the
                     // step) and no arrival count
@@ -102,7 +106,7 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
 // 16 KB instead of the 128 KB logits row for one block to read
 __global__ void __launch_bounds__(1024) argmax_parts_kernel(const ArgmaxPart* __restrict__ parts, int n,
                                                             int32_t* __restrict__ out,
-                                                            DecState* __restrict__ st) {
+                                                            DecState* __restrict__ st, int hist_off) {
     constexpr int NT = 1024, U = 4;
     const int tid = threadIdx.x;
     float best = -INFINITY;
@@ -118,7 +122,7 @@ __global__ void __launch_bounds__(1024) argmax_parts_kernel(const ArgmaxPart* __
         for (int u = 0; u < U; ++u)
             if (argmax_better(q[u].v, q[u].i, best, bi)) { best = q[u].v; bi = q[u].i; }
     }
-    argmax_finish(best, bi, out, st);
+    argmax_finish(best, bi, out, st, hist_off);
 }
 
 // row softmax (llama3.py:22-24): one wavefront per row, three passes over the row
@@ -192,8 +196,8 @@ hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out,
     return hipGetLastError();
 }
 hipError_t launch_argmax_parts(const ArgmaxPart* parts, int nparts, int32_t* out, hipStream_t s,
-                               DecState* st) {
-    hipLaunchKernelGGL(argmax_parts_kernel, dim3(1), dim3(1024), 0, s, parts, nparts, out, st);
+                               DecState* st, int hist_off) {
+    hipLaunchKernelGGL(argmax_parts_kernel, dim3(1), dim3(1024), 0, s, parts, nparts, out, st, hist_off);
     return hipGetLastError();
 }
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s) {

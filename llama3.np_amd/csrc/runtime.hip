@@ -173,6 +173,11 @@ struct l3_ctx {
     double step_us = 0.0;            // decode step time, host wall clock of synced steps (EMA)
     float* kv_bak = nullptr;         // [n_layers][KV_BAK_SLOTS][2: k, v][8][KVH][HD]
     bool bak_capture = false;        // run_layer: QKV launches keep the overwritten slot
+    // capture_steps, batch-1 argmax fold: the lm_head moves the position on (fold_adv), and the
+    // layer-0 QKV of every step after a graph's first reduces the previous step's fold_n lm_head
+    // partials itself (fold_in) instead of a separate argmax launch
+    bool fold_in = false, fold_adv = false;
+    int fold_n = 0;
     bool dec_bak = false;            // the captured single-step graph keeps it
     bool dec_n_bak = false;          // ... and the multi-step graph
     bool in_loop = false;            // generate_all drives the device state itself
@@ -625,6 +630,11 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     g.pos_dev = pos_dev;
     g.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     if (emb_ids) { g.A = c->emb; g.a_rows = emb_ids; }
+    if (emb_ids && c->fold_in) {  // the id comes from the previous step's lm_head partials
+        g.a_rows = nullptr;
+        g.amax_in = c->amax_part; g.amax_in_n = c->fold_n;
+        g.amax_ids = c->dec_ids; g.amax_st = c->dec_state;  // read by gate|up / O-proj below
+    }
     if (c->bak_capture) g.kv_bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD;
     // split-K workspace: one, for the GEMMs on c->stream (a batch split's parts keep > 256 rows,
     // past launch_split's range, so no two streams ever share it)
@@ -723,21 +733,41 @@ static GemmArgs lm_head_args(l3_ctx* c, int B, int L, float* logits_dev, int b0)
     return lm;
 }
 
+// batch 1 on the one-row GEMV: each lm_head block also leaves its (value, index) argmax, so a
+// greedy step's argmax reads those partials instead of the whole logits row (L3_LM_AMAX=0: off)
+static bool lm_amax_on() {
+    static const bool on = env_knob("L3_LM_AMAX", 1) != 0;
+    return on;
+}
+
 static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipStream_t s) {
     GemmArgs lm = lm_head_args(c, B, L, logits_dev, b0);
-    // batch 1 on the one-row GEMV: each block also leaves its (value, index) argmax, so a greedy
-    // step's argmax reads those partials instead of the whole logits row (L3_LM_AMAX=0: off)
-    static const bool amax_env = env_knob("L3_LM_AMAX", 1) != 0;
-    c->amax_n = amax_env && b0 == 0 ? gemv_store_blocks(lm) : 0;
+    c->amax_n = lm_amax_on() && b0 == 0 ? gemv_store_blocks(lm) : 0;
     if (c->amax_n) lm.amax_part = c->amax_part;
+    if (c->amax_n && c->fold_adv) lm.pos_adv = c->dec_state;
     return timed_on(c, L3_K_LMHEAD, s, [&] { return launch_gemm(EPI_STORE, lm, s); });
 }
 
 // greedy argmax of the rows the last forward left in c->logits (llama3.py:320): from the
-// lm_head's partials when it wrote them
-static hipError_t launch_greedy_argmax(l3_ctx* c, int B, DecState* st) {
-    if (c->amax_n && B == 1) return launch_argmax_parts(c->amax_part, c->amax_n, c->dec_ids, c->stream, st);
+// lm_head's partials when it wrote them; hist_off 1 when that lm_head moved the position on
+static hipError_t launch_greedy_argmax(l3_ctx* c, int B, DecState* st, int hist_off = 0) {
+    if (c->amax_n && B == 1) return launch_argmax_parts(c->amax_part, c->amax_n, c->dec_ids, c->stream, st, hist_off);
     return launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, st);
+}
+
+// partials the next step's layer-0 QKV reduces when a captured batch-1 step's argmax is folded
+// into it (0: no fold).  Every QKV block reads all of them, so only a small vocabulary's
+// (stories15M: 2000 partials, 16 KB; the Llama-3 shape's 32k keep the argmax launch).
+// L3_DECODE_FOLD_ARGMAX=0: off (A/B)
+static int fold_parts(l3_ctx* c, int B) {
+    static const bool on = env_knob("L3_DECODE_FOLD_ARGMAX", 1) != 0;
+    if (!on || B != 1 || !lm_amax_on() || !c->dec_state) return 0;
+    const int n = gemv_store_blocks(lm_head_args(c, 1, 1, c->logits, 0));
+    GemmArgs qkv{};
+    qkv.M = 1;
+    qkv.N = c->qkvn;
+    qkv.K = c->d.dim;
+    return n > 0 && n <= 4096 && gemv_direct(qkv) ? n : 0;
 }
 
 
@@ -908,13 +938,22 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
     c->timing = false;  // no event records inside the graph
     HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc = 0;
+    // batch 1: each step's argmax folded into the next step's layer-0 QKV, one argmax launch per
+    // graph (its last step); the lm_heads move the position on
+    const int fold = fold_parts(c, B);
     for (int i = 0; i < steps && !rc; ++i) {
+        c->fold_in = fold && i > 0;
+        c->fold_adv = fold > 0;
+        c->fold_n = fold;
         rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
-        if (!rc) {
-            hipError_t e = launch_greedy_argmax(c, B, c->dec_state);
+        c->fold_in = c->fold_adv = false;
+        if (!rc && fold && c->amax_n != fold) rc = fail("decode capture: lm_head partials %d, expected %d", c->amax_n, fold);
+        if (!rc && (!fold || i == steps - 1)) {
+            hipError_t e = launch_greedy_argmax(c, B, c->dec_state, fold ? 1 : 0);
             if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
         }
     }
+    c->fold_in = c->fold_adv = false;
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     c->timing = timing;

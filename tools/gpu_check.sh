@@ -63,6 +63,7 @@ for s in "$@"; do
     decgs32) L3_DECODE_GRAPH_STEPS=32 step decgs32 300 python tools/bench_decode.py ;;
     decspec0) L3_DECODE_SPECULATE=0 step decspec0 300 python tools/bench_decode.py ;;
     decamax0) L3_LM_AMAX=0 step decamax0 300 python tools/bench_decode.py ;;
+    decfold0) L3_DECODE_FOLD_ARGMAX=0 step decfold0 300 python tools/bench_decode.py ;;
     declayer0) L3_DECODE_LAYER=0 step declayer0 300 python tools/bench_decode.py ;;
     decnofuse) L3_DECODE_FUSE_O=0 step decnofuse 300 python tools/bench_decode.py ;;
     testsdec) step testsdec 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "greedy or generate or decode or head_dims or cli or cache_edges or tiny or golden or speculative or run_ahead" --timeout 300 --timeout-method thread ;;
