@@ -71,12 +71,41 @@ __device__ __forceinline__ int lds_swz(int r) {
 // buffer, k / v appended to the KV cache (llama3.py:184-185).  Branch-free over the q/k/v
 // sections (a V tile rotates by cos = 1, sin = 0, which is exact), and the RoPE table loads of
 // each row-half are issued before its stores: a load's vmcnt wait also waits for all older stores.
-template <int TM, int TN>
+// output column (the first of a lane's float4) -> q / k / v section, head, column in the head
+__device__ __forceinline__ void qkv_col(const GemmArgs& p, int col, int& sec, int& head, int& d) {
+    const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD;
+    sec = col < qdim ? 0 : (col < qdim + kvdim ? 1 : 2);
+    const int cc = col - (sec == 0 ? 0 : (sec == 1 ? qdim : qdim + kvdim));
+    head = cc / p.HD;
+    d = cc - head * p.HD;
+}
+
+// the RoPE table pairs of a one-row-tile QKV epilogue (TM = 1), fetched before the dot products
+// by a kernel that has them to spare (gemm_skinny_kernel): qkv_epilogue<1, TN, true> takes them
+template <int TN>
+__device__ __forceinline__ void qkv_tables(const GemmArgs& p, int mrow0, int ncol0, int lane,
+                                           float2 (&cs)[TN], float2 (&sn)[TN]) {
+    const int frow = lane & 15, fq4 = 4 * (lane >> 4);
+    const int rowc = min(mrow0 + frow, p.M - 1);
+    const int pos = start_of(p) + rowc - rowc / p.L * p.L;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        int sec, head, d;
+        qkv_col(p, min(ncol0 + j * 16 + fq4, p.N - 4) + p.col_base, sec, head, d);
+        const int t = pos * (p.HD >> 1) + (d >> 1);
+        cs[j] = *reinterpret_cast<const float2*>(p.rope_cos + t);
+        sn[j] = *reinterpret_cast<const float2*>(p.rope_sin + t);
+    }
+}
+
+template <int TM, int TN, bool PRE = false>
 __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&acc)[TM][TN],
                                              const float (&rs)[TM], int mrow0, int ncol0,
-                                             int lane) {
+                                             int lane, const float2* pre_cs = nullptr,
+                                             const float2* pre_sn = nullptr) {
+    static_assert(!PRE || TM == 1, "prefetched RoPE pairs: one row tile");
     const int frow = lane & 15, fq4 = 4 * (lane >> 4);
-    const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD, hd2 = p.HD >> 1;
+    const int qdim = p.H * p.HD, hd2 = p.HD >> 1;
     const int sp = start_of(p);
     int rowc[TM], bidx[TM], pos[TM];
 #pragma unroll
@@ -87,13 +116,7 @@ __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&ac
     }
     int sec[TN], head[TN], d[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int col = min(ncol0 + j * 16 + fq4, p.N - 4) + p.col_base;
-        sec[j] = col < qdim ? 0 : (col < qdim + kvdim ? 1 : 2);
-        const int cc = col - (sec[j] == 0 ? 0 : (sec[j] == 1 ? qdim : qdim + kvdim));
-        head[j] = cc / p.HD;
-        d[j] = cc - head[j] * p.HD;
-    }
+    for (int j = 0; j < TN; ++j) qkv_col(p, min(ncol0 + j * 16 + fq4, p.N - 4) + p.col_base, sec[j], head[j], d[j]);
     // two row-halves: each issues its RoPE loads (TM/2 x TN pairs) before its stores, so a
     // wave waits twice rather than once per float4, and the 4-block/CU register budget holds
     constexpr int TH = TM > 1 ? TM / 2 : 1;
@@ -104,9 +127,14 @@ __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&ac
         for (int ii = 0; ii < TH; ++ii)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int t = pos[i0 + ii] * hd2 + (d[j] >> 1);
-                cs[ii][j] = *reinterpret_cast<const float2*>(p.rope_cos + t);
-                sn[ii][j] = *reinterpret_cast<const float2*>(p.rope_sin + t);
+                if constexpr (PRE) {
+                    cs[ii][j] = pre_cs[j];
+                    sn[ii][j] = pre_sn[j];
+                } else {
+                    const int t = pos[i0 + ii] * hd2 + (d[j] >> 1);
+                    cs[ii][j] = *reinterpret_cast<const float2*>(p.rope_cos + t);
+                    sn[ii][j] = *reinterpret_cast<const float2*>(p.rope_sin + t);
+                }
             }
 #pragma unroll
         for (int ii = 0; ii < TH; ++ii) {
@@ -598,6 +626,21 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs p) {
     const float* wrow[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) wrow[j] = p.W + (int64_t)min(n0 + 16 * j + frow, p.N - 1) * p.K;
+    // the epilogue's own operands (EPI_RESID: the residual float4s of the lane's row; EPI_QKV: the
+    // RoPE table pairs) do not depend on the dot products: fetched now, with the fragments, not
+    // after the reduction (one memory round trip less per launch); every wave issues them, wave 0
+    // uses them (unpredicated: a wave-dependent branch would cost the others nothing but the
+    // waits hipcc places after it)
+    const int fq4 = 4 * (lane >> 4);
+    f32x4 res[EPI == EPI_RESID ? TN : 1];
+    float2 pcs[EPI == EPI_QKV ? TN : 1], psn[EPI == EPI_QKV ? TN : 1];
+    if constexpr (EPI == EPI_RESID) {
+        const float* rb = res_row(p, min(m0 + frow, p.M - 1));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) res[j] = *reinterpret_cast<const f32x4*>(rb + min(n0 + j * 16 + fq4, p.N - 4));
+    } else if constexpr (EPI == EPI_QKV) {
+        qkv_tables<TN>(p, m0, n0, lane, pcs, psn);
+    }
     f32x4 acc[1][TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -641,9 +684,10 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs p) {
         rs[0] = p.norm ? __builtin_amdgcn_rsqf(v * (1.0f / (float)p.K) + p.eps) : 1.0f;
     }
     if constexpr (EPI == EPI_QKV) {
-        qkv_epilogue<1, TN>(p, acc, rs, m0, n0, lane);
+        qkv_epilogue<1, TN, true>(p, acc, rs, m0, n0, lane, pcs, psn);
+    } else if constexpr (EPI == EPI_RESID) {
+        direct_epilogue<1, TN, EPI, true, TN>(p, acc, rs, res, m0, n0, lane);
     } else {
-        const f32x4 res[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
         direct_epilogue<1, TN, EPI, false, 1>(p, acc, rs, res, m0, n0, lane);
     }
 }
