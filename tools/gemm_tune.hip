@@ -255,6 +255,19 @@ int main(int argc, char** argv) {
                    GVAR(2, 3, 4, 4, EPI_SWIGLU, 2, 16)}, rounds, iters);
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "lmhead") {  // last-position lm_head tiles (C3 part / batched decode)
+        // M = 128 (a C3 batch-split part) and 256 (the batch, batched decode B = 256): one block
+        // per CU at the product tiles (250 / 500 blocks); smaller tiles put several on each CU
+        for (int m : {128, 256})
+            run_shape(m == 128 ? "lm_head M=128" : "lm_head M=256", EPI_STORE, m, 288, 32000, true,
+                      {m == 128 ? GVARN(2, 2, 4, 4, EPI_STORE, 2, 16, 4) : GVARN(4, 1, 4, 4, EPI_STORE, 2, 16, 3),
+                       GVARN(2, 2, 4, 2, EPI_STORE, 2, 16, 4), GVARN(2, 2, 2, 4, EPI_STORE, 2, 16, 4),
+                       GVARN(2, 2, 2, 4, EPI_STORE, 2, 16, 6), GVARN(2, 2, 2, 2, EPI_STORE, 4, 16, 4),
+                       GVARN(2, 2, 4, 2, EPI_STORE, 3, 16, 3), GVARN(1, 4, 4, 2, EPI_STORE, 2, 16, 4),
+                       GVARN(2, 2, 1, 4, EPI_STORE, 2, 16, 6)},
+                      rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "qkvepi") {  // what the QKV epilogue costs
         run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
                   {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(4, 1, 4, 6, EPI_QKV, 3, 16),
