@@ -43,6 +43,12 @@ struct Variant {
                 const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
                 hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, NS>), dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a); \
             }}
+// the skinny MFMA kernel (9-256 rows): a block per 16-row x 16*TN-column tile, 4 waves split K
+#define SVAR(EPI, TN, CH)                                                                             \
+    Variant{"skinny<tn" #TN ",ch" #CH ">", [](const GemmArgs& a, hipStream_t s) {                      \
+                const int64_t blocks = (int64_t)((a.M + 15) / 16) * ((a.N + 16 * TN - 1) / (16 * TN)); \
+                hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, CH>), dim3((unsigned)blocks), dim3(256), 0, s, a); \
+            }}
 #define RVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("regs", false, WM, WN, TM, TN, EPI, WPE, BK)
 #define GVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("glds", true, WM, WN, TM, TN, EPI, WPE, BK)
 
@@ -73,7 +79,7 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
     if (epi == EPI_QKV) {  // stories15M attention geometry: H = KVH = 6, HD = 48, L = 256
         g.H = 6; g.KVH = 6; g.HD = 48; g.L = 256; g.Smax = 256; g.start_pos = 0;
         g.q_scale = 0.2f;
-        const size_t cache = (size_t)(M / 256) * 6 * 256 * 48;
+        const size_t cache = (size_t)((M + 255) / 256) * 6 * 256 * 48;  // whole sequences of L = 256
         CK(hipMalloc(&qo, (size_t)M * 288 * 4)); CK(hipMalloc(&ck, cache * 4)); CK(hipMalloc(&cv, cache * 4));
         std::vector<float> tc(256 * 24), ts(256 * 24);
         fill(tc, -1.f, 1.f, 4); fill(ts, -1.f, 1.f, 5);
@@ -253,6 +259,29 @@ int main(int argc, char** argv) {
         run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
                   {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 3, 4, 4, EPI_SWIGLU, 3, 16),
                    GVAR(2, 3, 4, 4, EPI_SWIGLU, 2, 16)}, rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "skinny") {  // batched decode: the layer GEMMs at M = B
+        // (TN and CH do not change any element's K order: every variant is bit-identical)
+        for (int Ms : {64, 128, 256}) {
+            char l[64];
+            snprintf(l, sizeof l, "M=%d QKV", Ms);
+            run_shape(l, EPI_QKV, Ms, 288, 864, true,
+                      {SVAR(EPI_QKV, 1, 6), SVAR(EPI_QKV, 1, 2), SVAR(EPI_QKV, 1, 3), SVAR(EPI_QKV, 2, 2),
+                       SVAR(EPI_QKV, 2, 3), SVAR(EPI_QKV, 3, 2)}, rounds, iters);
+            snprintf(l, sizeof l, "M=%d gate|up", Ms);
+            run_shape(l, EPI_SWIGLU, Ms, 288, 1536, true,
+                      {SVAR(EPI_SWIGLU, 2, 6), SVAR(EPI_SWIGLU, 2, 1), SVAR(EPI_SWIGLU, 2, 2),
+                       SVAR(EPI_SWIGLU, 4, 1), SVAR(EPI_SWIGLU, 4, 2)}, rounds, iters);
+            snprintf(l, sizeof l, "M=%d O-proj", Ms);
+            run_shape(l, EPI_RESID, Ms, 288, 288, false,
+                      {SVAR(EPI_RESID, 1, 6), SVAR(EPI_RESID, 1, 2), SVAR(EPI_RESID, 1, 3), SVAR(EPI_RESID, 2, 2),
+                       SVAR(EPI_RESID, 2, 3)}, rounds, iters);
+            snprintf(l, sizeof l, "M=%d down", Ms);
+            run_shape(l, EPI_RESID, Ms, 768, 288, false,
+                      {SVAR(EPI_RESID, 1, 6), SVAR(EPI_RESID, 1, 2), SVAR(EPI_RESID, 1, 3), SVAR(EPI_RESID, 2, 2),
+                       SVAR(EPI_RESID, 2, 3), SVAR(EPI_RESID, 2, 4)}, rounds, iters);
+        }
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "lmhead") {  // last-position lm_head tiles (C3 part / batched decode)
