@@ -611,12 +611,12 @@ __global__ void __launch_bounds__(64 * WM * WN, WAVES_PER_EU) gemm_lds_kernel(Ge
 // four partial tiles (and row sums of squares) meet in LDS and wave 0 adds them in wave order
 // and runs the tiled kernel's epilogue (RMSNorm row factor, RoPE / KV append, SwiGLU pairs,
 // residual).  The weight-streaming GEMV keeps M <= 8, where its lanes' wider K split wins.
-template <int EPI, int TN, int CH>
-__global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs p) {
+template <int EPI, int TN, int CH, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) gemm_skinny_kernel(GemmArgs p) {
     static_assert(EPI != EPI_SWIGLU || TN % 2 == 0, "SwiGLU pairs gate / up tiles");
     constexpr int WN = 16 * TN;  // columns per tile
-    __shared__ f32x4 red[4][TN][64];
-    __shared__ float rss[4][64];
+    __shared__ f32x4 red[NW][TN][64];
+    __shared__ float rss[NW][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int frow = lane & 15, kq = 4 * (lane >> 4);
     const int ntn = (p.N + WN - 1) / WN;
@@ -646,7 +646,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs p) {
     for (int j = 0; j < TN; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     float ss = 0.f;
     const int nkb = p.K >> 4;
-    const int kb_lo = wid * nkb / 4, kb_hi = (wid + 1) * nkb / 4;  // this wave's k-blocks
+    const int kb_lo = wid * nkb / NW, kb_hi = (wid + 1) * nkb / NW;  // this wave's k-blocks
     for (int kb0 = kb_lo; kb0 < kb_hi; kb0 += CH) {
         f32x4 av[CH], wv[CH][TN];
 #pragma unroll
@@ -673,7 +673,7 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmArgs p) {
     __syncthreads();
     if (wid != 0) return;
 #pragma unroll
-    for (int w = 1; w < 4; ++w) {
+    for (int w = 1; w < NW; ++w) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[0][j] += red[w][j][lane];
         ss += rss[w][lane];

@@ -49,6 +49,11 @@ struct Variant {
                 const int64_t blocks = (int64_t)((a.M + 15) / 16) * ((a.N + 16 * TN - 1) / (16 * TN)); \
                 hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, CH>), dim3((unsigned)blocks), dim3(256), 0, s, a); \
             }}
+#define SVARW(EPI, TN, CH, NW)                                                                        \
+    Variant{"skinny<tn" #TN ",ch" #CH ",nw" #NW ">", [](const GemmArgs& a, hipStream_t s) {            \
+                const int64_t blocks = (int64_t)((a.M + 15) / 16) * ((a.N + 16 * TN - 1) / (16 * TN)); \
+                hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, CH, NW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a); \
+            }}
 #define RVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("regs", false, WM, WN, TM, TN, EPI, WPE, BK)
 #define GVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("glds", true, WM, WN, TM, TN, EPI, WPE, BK)
 
@@ -262,25 +267,30 @@ int main(int argc, char** argv) {
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "skinny") {  // batched decode: the layer GEMMs at M = B
-        // (TN and CH do not change any element's K order: every variant is bit-identical)
+        // waves per block (the K split): 4 (product) against 2 and 8 at the product's TN / CH;
+        // NW changes the partial sums, so the checks show rounding-level differences
         for (int Ms : {64, 128, 256}) {
             char l[64];
+            const bool wide = Ms > 128;
             snprintf(l, sizeof l, "M=%d QKV", Ms);
             run_shape(l, EPI_QKV, Ms, 288, 864, true,
-                      {SVAR(EPI_QKV, 1, 6), SVAR(EPI_QKV, 1, 2), SVAR(EPI_QKV, 1, 3), SVAR(EPI_QKV, 2, 2),
-                       SVAR(EPI_QKV, 2, 3), SVAR(EPI_QKV, 3, 2)}, rounds, iters);
+                      wide ? std::vector<Variant>{SVARW(EPI_QKV, 2, 2, 4), SVARW(EPI_QKV, 2, 2, 2), SVARW(EPI_QKV, 2, 2, 8), SVARW(EPI_QKV, 2, 1, 8)}
+                           : std::vector<Variant>{SVARW(EPI_QKV, 1, 2, 4), SVARW(EPI_QKV, 1, 2, 2), SVARW(EPI_QKV, 1, 2, 8), SVARW(EPI_QKV, 1, 1, 8)},
+                      rounds, iters);
             snprintf(l, sizeof l, "M=%d gate|up", Ms);
             run_shape(l, EPI_SWIGLU, Ms, 288, 1536, true,
-                      {SVAR(EPI_SWIGLU, 2, 6), SVAR(EPI_SWIGLU, 2, 1), SVAR(EPI_SWIGLU, 2, 2),
-                       SVAR(EPI_SWIGLU, 4, 1), SVAR(EPI_SWIGLU, 4, 2)}, rounds, iters);
+                      {SVARW(EPI_SWIGLU, 2, 2, 4), SVARW(EPI_SWIGLU, 2, 2, 2), SVARW(EPI_SWIGLU, 2, 2, 8), SVARW(EPI_SWIGLU, 2, 1, 8)},
+                      rounds, iters);
             snprintf(l, sizeof l, "M=%d O-proj", Ms);
             run_shape(l, EPI_RESID, Ms, 288, 288, false,
-                      {SVAR(EPI_RESID, 1, 6), SVAR(EPI_RESID, 1, 2), SVAR(EPI_RESID, 1, 3), SVAR(EPI_RESID, 2, 2),
-                       SVAR(EPI_RESID, 2, 3)}, rounds, iters);
+                      wide ? std::vector<Variant>{SVARW(EPI_RESID, 2, 2, 4), SVARW(EPI_RESID, 2, 2, 2), SVARW(EPI_RESID, 2, 2, 8), SVARW(EPI_RESID, 2, 1, 8)}
+                           : std::vector<Variant>{SVARW(EPI_RESID, 1, 2, 4), SVARW(EPI_RESID, 1, 2, 2), SVARW(EPI_RESID, 1, 2, 8), SVARW(EPI_RESID, 1, 1, 8)},
+                      rounds, iters);
             snprintf(l, sizeof l, "M=%d down", Ms);
             run_shape(l, EPI_RESID, Ms, 768, 288, false,
-                      {SVAR(EPI_RESID, 1, 6), SVAR(EPI_RESID, 1, 2), SVAR(EPI_RESID, 1, 3), SVAR(EPI_RESID, 2, 2),
-                       SVAR(EPI_RESID, 2, 3), SVAR(EPI_RESID, 2, 4)}, rounds, iters);
+                      wide ? std::vector<Variant>{SVARW(EPI_RESID, 2, 2, 4), SVARW(EPI_RESID, 2, 2, 2), SVARW(EPI_RESID, 2, 2, 8), SVARW(EPI_RESID, 2, 1, 8)}
+                           : std::vector<Variant>{SVARW(EPI_RESID, 1, 2, 4), SVARW(EPI_RESID, 1, 2, 2), SVARW(EPI_RESID, 1, 2, 8), SVARW(EPI_RESID, 1, 1, 8)},
+                      rounds, iters);
         }
         return 0;
     }
