@@ -294,6 +294,18 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "qkv18") {  // QKV wave tiles with more MFMAs per k-step
+        // 64 x 48 wave tiles issue 12 MFMAs per 4-deep k-step; 96 x 48 (192 x 96 blocks) 18 and
+        // 128 x 32 (3-wave 128 x 96 blocks) 16, both dividing N = 864 without padding
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(2, 2, 6, 3, EPI_QKV, 3, 16),
+                   GVAR(2, 2, 6, 3, EPI_QKV, 2, 16), GVAR(1, 3, 8, 2, EPI_QKV, 4, 16),
+                   GVAR(1, 3, 8, 2, EPI_QKV, 3, 16)}, rounds, iters);
+        run_shape("QKV shape, plain store", EPI_STORE, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_STORE, 4, 16), GVAR(2, 2, 6, 3, EPI_STORE, 3, 16),
+                   GVAR(1, 3, 8, 2, EPI_STORE, 4, 16)}, rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "lmhead") {  // last-position lm_head tiles (C3 part / batched decode)
         // M = 128 (a C3 batch-split part) and 256 (the batch, batched decode B = 256): one block
         // per CU at the product tiles (250 / 500 blocks); smaller tiles put several on each CU

@@ -31,6 +31,7 @@ for s in "$@"; do
     tunering) step tunering 600 tools/gemm_tune 5 10 ring ;;
     tunelm) step tunelm 300 tools/gemm_tune 5 20 lmhead ;;
     tunesk) step tunesk 300 tools/gemm_tune 5 50 skinny ;;
+    tuneqkv18) step tuneqkv18 300 tools/gemm_tune 5 10 qkv18 ;;
     tunec5) step tunec5 900 tools/gemm_tune 3 3 c5 ;;
     pmcsq) step pmcA 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcA -o run --output-format csv -- tools/attn_tune 1 2
            step pmcB 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcB -o run --output-format csv -- tools/attn_tune 1 2
