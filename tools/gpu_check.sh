@@ -81,6 +81,7 @@ for s in "$@"; do
     c4) step c4 300 python bench.py --global-batch 2048 --steps 5 --warmup 1 --no-cpu-baseline --no-kernel-breakdown ;;
     c5dec) step c5dec 600 python bench.py --workload c5decode --steps 30 ;;
     c5decnt0) L3_GEMV_NT=0 step c5decnt0 600 python bench.py --workload c5decode --steps 30 ;;
+    c5declpu*) L3_GEMV_LPU=${s#c5declpu} step $s 600 python bench.py --workload c5decode --steps 30 ;;
     c5decsk0) L3_SPLITK=0 step c5decsk0 600 python bench.py --workload c5decode --steps 30 ;;
     c5decb*) L3_SPLITK_BLOCKS=${s#c5decb} step $s 600 python bench.py --workload c5decode --steps 30 ;;
     c5deckt*) L3_SPLITK_MINKT=${s#c5deckt} step $s 600 python bench.py --workload c5decode --steps 30 ;;
