@@ -65,7 +65,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_ranks(n, argv, cmd=None, timeout_s=None, grace_s=20.0, out=None):
+def spawn_ranks(n, argv, cmd=None, timeout_s=1800.0, grace_s=20.0, out=None):
     """``--gpus N`` with no launcher (WORLD_SIZE unset): start N fresh rank processes, one per
     GPU, the way torch.distributed.run would, and wait for them.
 
@@ -77,7 +77,12 @@ def spawn_ranks(n, argv, cmd=None, timeout_s=None, grace_s=20.0, out=None):
     ranks' stdout goes to stderr.  If any rank fails, the ranks still running are given
     ``grace_s`` and then killed by pid (a peer blocked in an RCCL call never returns on its
     own), and the first failing rank's exit status is returned; 0 when every rank succeeded.
+    ``timeout_s`` (default 30 min, ``--spawn-timeout``; None: no limit) bounds the whole launch
+    (every rank hung together, e.g. in RCCL init, returns 124).  On any exit path — a
+    KeyboardInterrupt or SIGTERM in this process included — every child still running is killed
+    by pid and reaped, so no rank is left holding its GPU.
     ``cmd`` (tests) replaces the rank body ``[python, bench.py] + argv``."""
+    import signal
     import subprocess
     import uuid
 
@@ -86,32 +91,46 @@ def spawn_ranks(n, argv, cmd=None, timeout_s=None, grace_s=20.0, out=None):
     base = list(cmd) if cmd else [sys.executable, "-u", os.path.abspath(__file__)]
     out = sys.stdout if out is None else out
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), L3_LAUNCH_KEY=key)
-        procs.append(subprocess.Popen(base + list(argv), env=env,
-                                      stdout=out if r == 0 else sys.stderr))
-    t0 = time.time()
-    first_bad, bad_at = None, None
-    while True:
-        rcs = [p.poll() for p in procs]
-        for r, rc in enumerate(rcs):
-            if rc not in (None, 0) and first_bad is None:
-                first_bad, bad_at = (r, rc), time.time()
-        if all(rc is not None for rc in rcs):
-            break
-        late = timeout_s is not None and time.time() - t0 > timeout_s
-        if late or (bad_at is not None and time.time() - bad_at > grace_s):
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()  # the exact child pid this function started
-            for p in procs:
-                p.wait()
-            if first_bad is None:
-                first_bad = (-1, 124)
-            break
-        time.sleep(0.05)
+
+    def _term(signum, frame):  # SIGTERM -> the finally below reaps the ranks
+        raise SystemExit(128 + signum)
+
+    old_term = None
+    try:
+        old_term = signal.signal(signal.SIGTERM, _term)
+    except ValueError:  # not the main thread: the finally still covers KeyboardInterrupt
+        pass
+    first_bad = None
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(port), L3_LAUNCH_KEY=key)
+            procs.append(subprocess.Popen(base + list(argv), env=env,
+                                          stdout=out if r == 0 else sys.stderr))
+        t0 = time.time()
+        bad_at = None
+        while True:
+            rcs = [p.poll() for p in procs]
+            for r, rc in enumerate(rcs):
+                if rc not in (None, 0) and first_bad is None:
+                    first_bad, bad_at = (r, rc), time.time()
+            if all(rc is not None for rc in rcs):
+                break
+            late = timeout_s is not None and time.time() - t0 > timeout_s
+            if late or (bad_at is not None and time.time() - bad_at > grace_s):
+                if first_bad is None:
+                    first_bad = (-1, 124)
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()  # the exact child pid this function started
+        for p in procs:
+            p.wait()
+        if old_term is not None:
+            signal.signal(signal.SIGTERM, old_term)
     if first_bad is not None:
         r, rc = first_bad
         print(json.dumps({"error": "rank failed" if r >= 0 else "ranks timed out", "rank": r,
@@ -139,8 +158,12 @@ class Dist:
     def comm(self):
         return self.world > 1 or self.force_comm
 
-    def init_comm(self, ctx):
+    def init_comm(self, ctx, overlap=False):
+        """Communicator up, then what RCCL saw (ncclCommCount, every rank's PCI bus id gathered
+        over RCCL itself): every rank checks it (check_devices), so a run that is not N ranks on
+        N distinct GPUs stops on every rank at once, before any timed step."""
         self.ctx = ctx
+        self.info = None
         if self.world > 1 or self.force_comm:
             key = l3hip.launch_key()
             uid = l3hip.exchange_unique_id(self.rank, self.world, key)
@@ -148,6 +171,12 @@ class Dist:
             ctx.comm_barrier()
             if self.rank == 0:  # every rank has read the id once the communicator is up
                 l3hip.remove_unique_id(key)
+            if overlap:
+                ctx.set_comm_overlap(True)
+            info = ctx.comm_info()
+            self.info = check_devices(info["nranks"], self.world, info["busids"], info["rank"],
+                                      self.rank)
+            self.info["comm_mode"] = "overlapped" if overlap else "serialized"
 
     def barrier(self):
         if self.comm:
@@ -155,6 +184,51 @@ class Dist:
 
     def max(self, x):
         return self.ctx.comm_max(x) if self.comm else x
+
+    def min(self, x):
+        return -self.ctx.comm_max(-x) if self.comm else x
+
+
+class SingleProcess:
+    """--single-process: this one process drives N GPUs through l3hip.Group (ncclCommInitAll,
+    one thread, one grouped gather per step); barriers and max-over-ranks are local."""
+
+    def __init__(self, n):
+        if "WORLD_SIZE" in os.environ and os.environ["WORLD_SIZE"] != "1":
+            raise SystemExit("--single-process drives every GPU from one process: no launcher")
+        self.world, self.rank, self.local_rank, self.comm = n, 0, 0, n > 1
+        self.info = None
+
+    def barrier(self):
+        pass
+
+    def max(self, x):
+        return x
+
+    def min(self, x):
+        return x
+
+
+def check_devices(nranks, world, busids, rank_seen, rank):
+    """The N > 1 proof the driver's scaling line needs: RCCL's own rank count equals WORLD_SIZE,
+    it numbers this process as RANK, and every rank sits on a distinct PCI device.  Returns the
+    fields for the JSON line; raises SystemExit(4) otherwise (every rank sees the same gathered
+    list, so every rank stops)."""
+    errs = []
+    if nranks != world:
+        errs.append(f"RCCL counts {nranks} ranks, WORLD_SIZE is {world}")
+    if rank_seen != rank:
+        errs.append(f"RCCL numbers this process {rank_seen}, RANK is {rank}")
+    if len(busids) != nranks:
+        errs.append(f"{len(busids)} bus ids for {nranks} ranks")
+    dup = sorted({b for b in busids if busids.count(b) > 1})
+    if dup:
+        errs.append(f"ranks share a device: {dup}")
+    if errs:
+        print(json.dumps({"error": "multi-GPU device check failed", "details": errs,
+                          "rccl_nranks": nranks, "devices": busids}), flush=True)
+        raise SystemExit(4)
+    return {"rccl_nranks": nranks, "devices": list(busids)}
 
 
 def cpu_baseline():
@@ -207,7 +281,9 @@ def cpu_baseline():
             one = round(B1 * SEQ / (time.perf_counter() - t1), 1)
     except Exception:
         pass
-    return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(blas),
+    # "cores" is the contract's name for the threads actually used (one OpenBLAS thread per core
+    # it runs on); "threads" says the same under its plain name
+    return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(blas), "threads": int(blas),
             "nproc": os.cpu_count(), "affinity": affinity, "openblas_threads": int(blas),
             "thread_cap": cap,
             "value_1_thread_sample": one,
@@ -453,6 +529,33 @@ def check_gathered(ctx, dist, bpg, VS, gathered_dev):
     return dist.world
 
 
+def check_gathered_group(ctx, N, bpg, VS, gathered_dev, ids_blk):
+    """--single-process self-check (untimed): member r's rows (global rows r, r + N, ...) of the
+    last gathered step against member 0's own recomputation of member r's id block — same B,
+    same kernels, so bit-identical.  Returns N; SystemExit(3) on a mismatch."""
+    got = np.empty((bpg * N, VS), np.float32)
+    ctx.d2h(got, gathered_dev)
+    ids_dev = ctx.alloc(bpg * SEQ * 4)
+    out_dev = ctx.alloc(bpg * VS * 4)
+    want = np.empty((bpg, VS), np.float32)
+    try:
+        for r in range(N):
+            ctx.h2d(ids_dev, ids_blk[r])
+            ctx.forward_dev(ids_dev, bpg, SEQ, 0, out_dev)
+            ctx.d2h(want, out_dev)
+            blk = got[r::N]
+            if not np.array_equal(blk, want):
+                bad = np.argwhere(blk != want)
+                print(json.dumps({"error": "gathered logits differ from member 0's recomputation",
+                                  "member": r, "mismatches": int(bad.shape[0]),
+                                  "first": bad[0].tolist()}), flush=True)
+                raise SystemExit(3)
+    finally:
+        ctx.free(ids_dev)
+        ctx.free(out_dev)
+    return N
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -475,14 +578,22 @@ def main():
     ap.add_argument("--rccl", action="store_true",
                     help="communicator, gather and self-check even at N=1 (rehearses the N>1 path "
                          "under torch.distributed.run --nproc-per-node 1)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives all N GPUs (l3hip.Group: ncclCommInitAll, one thread, "
+                         "one grouped RCCL gather per step) instead of one process per GPU")
+    ap.add_argument("--comm-overlap", action="store_true",
+                    help="the overlapped gather (l3_comm_set_overlap): the next step's second batch "
+                         "part runs during the gather (default: serialized)")
+    ap.add_argument("--spawn-timeout", type=float, default=1800.0,
+                    help="seconds before spawned ranks still running are killed (0: no limit)")
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank processes here even at N=1 (rehearses the launcher-free "
                          "N>1 path; N>1 without WORLD_SIZE spawns anyway)")
     a = ap.parse_args()
-    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.spawn):
+    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.spawn) and not a.single_process:
         # no launcher: this process only starts the ranks (nothing here has touched the GPU)
         argv = [x for x in sys.argv[1:] if x != "--spawn"]
-        raise SystemExit(spawn_ranks(a.gpus, argv))
+        raise SystemExit(spawn_ranks(a.gpus, argv, timeout_s=a.spawn_timeout or None))
     if a.workload == "c5":
         return bench_c5(a)
     if a.workload == "c5cpu":
@@ -490,7 +601,7 @@ def main():
     if a.workload == "c5decode":
         return bench_c5_decode(a)
 
-    dist = Dist(a.gpus, force_comm=a.rccl)
+    dist = SingleProcess(a.gpus) if a.single_process else Dist(a.gpus, force_comm=a.rccl)
     # default: weak scaling, B = 256 rows per GPU (N = 8 is C4's B = 2048); --global-batch G:
     # strong scaling, G rows split over the N GPUs (C4 at any N)
     if a.global_batch:
@@ -499,6 +610,7 @@ def main():
         bpg = a.global_batch // dist.world
     else:
         bpg = B_PER_GPU
+    N = dist.world
     dev = dist.local_rank
     args = synth.stories15m(bpg)
     FD, D = synth.STORIES15M_HIDDEN, args.dim
@@ -506,75 +618,109 @@ def main():
     with tempfile.TemporaryDirectory() as tmp:
         path = os.path.join(tmp, "stories15m_synth.npz")
         synth.save_npz(path, weights)
-        model = llama3.Llama(path, args, device=dev)
+        if a.single_process:  # one process, N devices: l3hip.Group under Llama(devices=...)
+            model = llama3.Llama(path, synth.stories15m(bpg * N), devices=list(range(N)))
+        else:
+            model = llama3.Llama(path, args, device=dev)
     ctx = model.context
+    members = model.group.members if a.single_process else [ctx]
     VS = args.vocab_size
 
-    # inputs resident in HBM before the timed region
-    ids = np.random.default_rng(100 + dist.rank).integers(0, VS, (bpg, SEQ)).astype(np.int32)
-    ids_dev = ctx.alloc(ids.nbytes)
-    ctx.h2d(ids_dev, ids)
+    # inputs resident in HBM before the timed region: rank (member) r's rows are the seeded
+    # block default_rng(100 + r); single-process: member r holds global rows r, r + N, ...
+    ids_blk = [np.random.default_rng(100 + r).integers(0, VS, (bpg, SEQ)).astype(np.int32)
+               for r in (range(N) if a.single_process else [dist.rank])]
+    ids_devs = []
+    for m, blk in zip(members, ids_blk):
+        ids_devs.append(m.alloc(blk.nbytes))
+        m.h2d(ids_devs[-1], blk)
+    ids_dev = ids_devs[0]
     logits_dev = ctx.alloc(bpg * VS * 4)
     gathered_dev = None
-    rows = [bpg] * dist.world
-    dist.init_comm(ctx)
+    rows = [bpg] * N
+    if not a.single_process:
+        dist.init_comm(ctx, overlap=a.comm_overlap)
     if dist.comm and dist.rank == 0:
-        gathered_dev = ctx.alloc(bpg * dist.world * VS * 4)
-
+        gathered_dev = ctx.alloc(bpg * N * VS * 4)
     step_gather = dist.comm and not a.no_step_gather
 
-    def step():
-        ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
-        if step_gather:
-            ctx.gather_logits(logits_dev, gathered_dev, rows, root=0)
+    if a.single_process:
+        info = [m.comm_info(gather_busids=False) for m in members]
+        busids = members[0].comm_info()["busids"]
+        for r, x in enumerate(info):
+            check_devices(x["nranks"], N, busids, x["rank"], r)
+        dist.info = {"rccl_nranks": info[0]["nranks"], "devices": busids,
+                     "comm_mode": "single-process group (ncclCommInitAll, one thread)"}
+
+        def step():
+            if N > 1:
+                model.group.forward_dev(ids_devs, bpg * N, SEQ, 0, gathered_dev)
+            else:
+                ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
+
+        sync = model.group.synchronize
+    else:
+        def step():
+            ctx.forward_dev(ids_dev, bpg, SEQ, 0, logits_dev)
+            if step_gather:
+                ctx.gather_logits(logits_dev, gathered_dev, rows, root=0)
+
+        sync = ctx.synchronize
+
+    def each(fn):
+        for m in members:
+            fn(m)
 
     if a.split is not None:
-        ctx.set_batch_split(a.split)
+        each(lambda m: m.set_batch_split(a.split))
 
     def timed_steps(steps):
         dist.barrier()
-        ctx.synchronize()
+        sync()
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
-        ctx.synchronize()
+        sync()
         el = time.perf_counter() - t0
         dist.barrier()
-        return dist.max(el)
+        return dist.max(el), dist.min(el)
 
     for _ in range(a.warmup):
         step()
-    ctx.synchronize()
+    sync()
     # value: the product forward (batch split into row ranges on concurrent streams), no events
-    elapsed = timed_steps(a.steps)
+    elapsed, elapsed_min = timed_steps(a.steps)
 
     # N > 1: the gathered rows against rank 0's own recomputation (untimed)
-    checked = check_gathered(ctx, dist, bpg, VS, gathered_dev) if step_gather else None
+    if a.single_process:
+        checked = check_gathered_group(ctx, N, bpg, VS, gathered_dev, ids_blk) if N > 1 else None
+    else:
+        checked = check_gathered(ctx, dist, bpg, VS, gathered_dev) if step_gather else None
     dist.barrier()
 
     # beside `value`: the same K steps with the last block run on every position (the product
     # runs its attention / O-proj / FFN on each sequence's last position only: the rows that
     # reach the logits; l3_set_last_layer_rows) — and every pass below counts full layers
-    ctx.set_last_layer_rows(True)
+    each(lambda m: m.set_last_layer_rows(True))
     step()
-    elapsed_all_rows = timed_steps(a.steps)
+    elapsed_all_rows, _ = timed_steps(a.steps)
 
     # roofline: the same K steps serialized (one row range, one stream) with HIP events around
     # the FFN GEMM launches only (12 per step) — with concurrent row ranges two kernels share
     # the CUs and a launch's duration no longer measures that kernel
-    ctx.set_batch_split(1)
+    each(lambda m: m.set_batch_split(1))
     step()
     ctx.kernel_timing(True, ["gateup", "down"])
-    elapsed_serial = timed_steps(a.steps)
+    elapsed_serial, _ = timed_steps(a.steps)
     stats = ctx.kernel_stats()
     ctx.kernel_timing(False)
-    ctx.set_batch_split(a.split if a.split is not None else 2)
-    ctx.set_last_layer_rows(False)
+    each(lambda m: m.set_batch_split(a.split if a.split is not None else 2))
+    each(lambda m: m.set_last_layer_rows(False))
 
     # N > 1: the logits gather alone (untimed for `value`): its share of a step at this N,
     # which the overlapped gather hides behind the next step's layers
     gather_ms = None
-    if dist.comm:
+    if dist.comm and not a.single_process:
         dist.barrier()
         ctx.synchronize()
         t0 = time.perf_counter()
@@ -586,7 +732,12 @@ def main():
     # the drop-in host path, Llama.__call__ on host ids (int64) returning host
     # logits (a pinned NumPy array): ids H2D + forward + logits D2H (PCIe-inclusive; reported
     # beside `value`, never as it)
-    ids_host = ids.astype(np.int64)
+    if a.single_process:  # the global batch: row r + N*j is member r's row j
+        ids_host = np.empty((bpg * N, SEQ), np.int64)
+        for r, blk in enumerate(ids_blk):
+            ids_host[r::N] = blk
+    else:
+        ids_host = ids_blk[0].astype(np.int64)
     d2h_steps = max(1, min(a.steps, 10))
     out = model(ids_host, 0)
     del out
@@ -599,7 +750,7 @@ def main():
 
     # sanity on the output (outside the timed region)
     probe = np.empty((2, VS), np.float32)
-    ctx.d2h(probe, logits_dev)
+    ctx.d2h(probe, gathered_dev if a.single_process and N > 1 else logits_dev)
     if not np.isfinite(probe).all():
         raise SystemExit("non-finite logits")
 
@@ -629,6 +780,11 @@ def main():
         "batch_split": a.split if a.split is not None else 2,
         "ms_per_step_with_logits_d2h": round(host_ms, 4),
         "host_path_tokens_per_s": round(T * dist.world * d2h_steps / elapsed_d2h, 1),
+        "ms_per_step_rank_min": round(elapsed_min / a.steps * 1e3, 4),
+        "ms_per_step_rank_max": round(elapsed / a.steps * 1e3, 4),
+        "launcher": "single-process" if a.single_process else (
+            "spawned" if os.environ.get("L3_LAUNCH_KEY", "").startswith("spawn_") else
+            "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "none"),
         "ms_gather_alone": None if gather_ms is None else round(gather_ms, 4),
         "gather_self_check_ranks": checked,
         "higher_is_better": True,
@@ -640,6 +796,7 @@ def main():
                    "global_batch": bpg * dist.world, "seq_len": SEQ,
                    "parallelism": f"dp{dist.world} (batch rows) + RCCL logits gather"},
         "lib": {"version": l3hip.version(), "source_hash": l3hip.source_hash()},
+        **(dist.info or {}),
         "roofline": {"kernel": f"gemm gate|up (fused SwiGLU epilogue), M={T} K=288 N=1536",
                      "pass": "same workload and step count, batch split off (HIP events need "
                              "the kernel alone on the CUs)",
@@ -658,6 +815,7 @@ def main():
         ctx.kernel_timing(True)
         for _ in range(3):
             step()
+        sync()
         out["kernel_ms"] = {k: round(v[0] / v[1], 4) for k, v in ctx.kernel_stats().items() if v[1]}
         ctx.kernel_timing(False)
     print(json.dumps(out))

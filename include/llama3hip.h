@@ -208,21 +208,37 @@ int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits
 int l3_set_decode_horizon(l3_ctx* ctx, int32_t end_pos);
 
 /* ---- multi-GPU: batch-sharded prefill + RCCL logits gather (xGMI) -------- */
+/* The reference never mixes batch rows (llama3.py:163-211), so the batch axis shards with no
+ * exchange until the last-position logits (llama3.py:304-307), which one RCCL gather brings to
+ * the root.  Two ways to drive it: one process per GPU (l3_comm_*, what torch.distributed.run
+ * launches) or one process driving N devices (l3_group_*, below). */
+#define L3_BUSID_LEN 16  /* PCI bus id "dddd:bb:dd.f" + NUL, as hipDeviceGetPCIBusId writes it */
 /* 128-byte RCCL unique id (rank 0 creates, every rank receives it). */
 int l3_comm_unique_id(uint8_t id_out[128]);
 int l3_comm_init(l3_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t id[128]);
+/* What RCCL reports for this rank — ncclCommCount (nranks), ncclCommUserRank (rank),
+ * ncclCommCuDevice (device) — and every rank's PCI bus id, all-gathered over the communicator
+ * into busids [nranks][L3_BUSID_LEN] (busids_cap entries of room; NULL: skip the gather).
+ * Collective when busids is given: every rank calls it.  Without a communicator: 1 rank, this
+ * device.  Lets a multi-GPU run prove it ran N ranks on N distinct devices. */
+int l3_comm_info(l3_ctx* ctx, int32_t* nranks, int32_t* rank, int32_t* device, char* busids,
+                 int64_t busids_cap);
+/* on != 0: the overlapped gather form below (default off: serialized). */
+int l3_comm_set_overlap(l3_ctx* ctx, int32_t on);
 /* Gather each rank's logits rows [rows_r, VS] (device) into root's dst_dev
  * [sum rows, VS] in rank order; rows_per_rank has nranks entries.  Async, on
- * the context stream, after the forward that wrote src.  When the next call is
- * l3_forward_dev with its batch split, that forward's second part starts from
- * the point before the gather (its layers overlap the transfer), its first part
- * runs after the gather, and every part's lm_head waits for it (it reads the
- * rows the lm_head rewrites); any other entry point runs after the gather.  An
- * l3_d2h of dst_dev or l3_synchronize sees the gathered rows.  Calls of one
- * step must be made in the same order on every rank (RCCL point-to-point:
- * one grouped ncclRecv per peer on the root, one ncclSend per non-root rank).
- * Env L3_COMM_MODE (A/B only): 3 the form above (default), 1 the gather fully
- * serialized on the context stream, 0 a comm stream ordered by events
+ * the context stream, after the forward that wrote src; any later call runs
+ * after it.  An l3_d2h of dst_dev or l3_synchronize sees the gathered rows.
+ * Calls of one step must be made in the same order on every rank (RCCL
+ * point-to-point: one grouped ncclRecv per peer on the root, one ncclSend per
+ * non-root rank).  Only for contexts with their own communicator (l3_comm_init):
+ * a group's members gather through l3_group_* (one thread, all ranks in one
+ * RCCL group).  l3_comm_set_overlap(ctx, 1) takes the overlapped form: when
+ * the next call is l3_forward_dev with its batch split, that forward's second
+ * part starts from the point before the gather (its layers overlap the
+ * transfer), its first part runs after the gather, and every part's lm_head
+ * waits for it (it reads the rows the lm_head rewrites).  Env L3_COMM_MODE (A/B
+ * only): 1 serialized (default), 3 overlapped, 0 a comm stream ordered by events
  * (measured slower, DESIGN.md Multi-GPU). */
 int l3_comm_gather_logits(l3_ctx* ctx, const float* src_dev, float* dst_dev,
                           const int64_t* rows_per_rank, int32_t root);
@@ -236,6 +252,44 @@ int l3_comm_gather_argmax(l3_ctx* ctx, const float* logits_dev, int32_t* ids_dst
 int l3_comm_barrier(l3_ctx* ctx);
 /* max over ranks of one host double (in place; synchronous) — e.g. step time */
 int l3_comm_allreduce_max(l3_ctx* ctx, double* value);
+
+/* ---- one process, N devices (SURVEY 8(b) l3_group_*) -------------------
+ * The single-process drop-in of Llama.__call__ / Llama.generate (llama3.py:285-321) over the
+ * GPUs of a node: one context per device, communicators from ncclCommInitAll, every call
+ * launched asynchronously on all devices from one thread, one grouped RCCL gather, one sync.
+ * Batch row r lives on member r % n as its local row r / n (a mapping that does not depend on B,
+ * so each row's KV cache stays on one device across calls of any batch size, exactly as the
+ * reference's cache row r persists, llama3.py:138-153,184-187); each member's max_batch_size is
+ * ceil(max_batch_size / n).  Rows on one device only (B = 1: single-prompt greedy decode) run
+ * that member's own single-device path (graph-replayed decode steps).  Results are the
+ * single-device forward's: every member runs the same kernels on its rows (rows never interact);
+ * each row's logits are bit-identical to a single-device run of the same rows whenever both
+ * pick the same kernels for their row counts (every prefill of more than 256 tokens per part). */
+typedef struct l3_group l3_group;
+/* devices: n device ordinals (distinct); dims: the model, max_batch_size the global batch. */
+int l3_group_create(int32_t ndev, const int32_t* devices, const l3_dims* dims, l3_group** out);
+int l3_group_destroy(l3_group* g);
+/* member i's context (owned by the group: never l3_destroy it); for per-device buffers,
+ * timing and settings (l3_set_batch_split, l3_kernel_timing, ...). */
+int l3_group_context(l3_group* g, int32_t i, l3_ctx** ctx);
+/* l3_upload_weight / l3_finalize on every member. */
+int l3_group_upload_weight(l3_group* g, int32_t layer, int32_t kind, const float* host, int64_t rows,
+                           int64_t cols);
+int l3_group_finalize(l3_group* g);
+/* Llama.__call__ (llama3.py:285-308): ids [B, L] int64 host -> logits_host [B, VS] fp32 in
+ * row order.  Each member uploads and runs its rows, the root (member 0) receives the others'
+ * rows over RCCL and copies the assembled rows back. */
+int l3_group_forward_host(l3_group* g, const int64_t* ids_host, int32_t B, int32_t L,
+                          int32_t start_pos, float* logits_host);
+/* Device-resident form (bench): ids_dev[i] = member i's rows (int32 [B_i, L], rows i, i + n, ...,
+ * on device i), logits_dev = [B, VS] on member 0 in row order.  Async; l3_group_synchronize. */
+int l3_group_forward_dev(l3_group* g, const int32_t* const* ids_dev, int32_t B, int32_t L,
+                         int32_t start_pos, float* logits_dev);
+/* One greedy step (llama3.py:313-320): forward + argmax per member (first index on ties),
+ * only the B int32 ids gathered.  next_ids_host [B] int64. */
+int l3_group_greedy_step_host(l3_group* g, const int64_t* ids_host, int32_t B, int32_t L,
+                              int32_t start_pos, int64_t* next_ids_host);
+int l3_group_synchronize(l3_group* g);
 
 #ifdef __cplusplus
 }

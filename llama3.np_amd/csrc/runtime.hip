@@ -131,14 +131,20 @@ struct l3_ctx {
     // rccl
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
-    // comm stream of the A/B gather mode 0 (the default mode 3 gathers on stream, see
+    bool comm_owned = true;          // false: the communicator belongs to an l3_group
+    l3_group* group = nullptr;       // the group this context is a member of (l3_group_create)
+    // logits gather form (l3_comm_set_overlap; env L3_COMM_MODE for A/B): 1 serialized on the
+    // context stream (default), 3 the next forward's second batch part overlapping the gather,
+    // 0 a comm stream ordered by events (measured slower)
+    int comm_mode = 1;
+    // comm stream of the A/B gather mode 0 (modes 1 and 3 gather on stream, see
     // l3_comm_gather_logits); the next lm_head (the writer of the gathered rows) waits for the
     // gather, every other entry point joins it first (set_dev)
     hipStream_t comm_stream = nullptr;
     int32_t* gather_ids = nullptr;   // [maxB] this rank's argmax ids (l3_comm_gather_argmax)
     hipEvent_t comm_fwd_ev = nullptr, comm_done_ev = nullptr;
     bool gather_pending = false;
-    // mode 3 (L3_COMM_MODE): the gather was the last work queued on stream, and comm_fwd_ev marks
+    // mode 3 (l3_comm_set_overlap): the gather was the last work queued on stream, and comm_fwd_ev marks
     // the stream just before it — the next l3_forward_dev's second batch part starts from there,
     // so its layers overlap the transfer (only that entry point keeps the flag: set_dev clears it)
     bool gather_tail = false;
@@ -170,7 +176,10 @@ struct l3_ctx {
     // 16 steps at stories15M's 0.1 ms, none at the Llama-3-8B shape's 5 ms per step.
     static constexpr int SPEC_AHEAD = 16;
     static constexpr double SPEC_BUDGET_US = 4000.0;
-    double step_us = 0.0;            // decode step time, host wall clock of synced steps (EMA)
+    double step_us = 0.0;            // decode step time (EMA): graph replays (host wall clock of a
+                                     // synced replay, HIP events around each queued run-ahead graph)
+    bool step_us_seed = false;       // step_us is still the eager first step's (an upper bound):
+                                     // the first replay's time replaces it
     float* kv_bak = nullptr;         // [n_layers][KV_BAK_SLOTS][2: k, v][8][KVH][HD]
     bool bak_capture = false;        // run_layer: QKV launches keep the overwritten slot
     // capture_steps, batch-1 argmax fold: the lm_head moves the position on (fold_adv), and the
@@ -188,9 +197,11 @@ struct l3_ctx {
     int spec_base = 0, spec_end = 0; // queued steps cover positions [spec_base, spec_end)
     int spec_B = 0;
     int spec_limit = 0x7fffffff;     // l3_set_decode_horizon: no step at or past this position
-    struct SpecChunk { int pos0, n; hipEvent_t ev; bool done; };
+    // ev0 / ev1 bracket the chunk's graph launch (its device time keeps step_us current while
+    // steps are served from the queue), ev follows the ids copy (the chunk is ready)
+    struct SpecChunk { int pos0, n; hipEvent_t ev0, ev1, ev; bool done; };
     std::deque<SpecChunk> spec_q;
-    std::vector<hipEvent_t> spec_free;  // event pool
+    std::vector<hipEvent_t> spec_free;  // event pool (timing events)
     int64_t spec_hits = 0;
 };
 
@@ -398,7 +409,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->comm && c->comm_owned) ncclCommDestroy(c->comm);
     if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
     if (c->comm_fwd_ev) (void)hipEventDestroy(c->comm_fwd_ev);
     if (c->comm_done_ev) (void)hipEventDestroy(c->comm_done_ev);
@@ -416,7 +427,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     drop_decode_graph(c);
     dfree(c->dec_ids); dfree(c->dec_state); dfree(c->kv_bak);
     if (c->dec_host) (void)hipHostFree(c->dec_host);
-    for (auto& q : c->spec_q) (void)hipEventDestroy(q.ev);
+    for (auto& q : c->spec_q) { (void)hipEventDestroy(q.ev0); (void)hipEventDestroy(q.ev1); (void)hipEventDestroy(q.ev); }
     for (hipEvent_t e : c->spec_free) (void)hipEventDestroy(e);
     dfree(c->spec_hist);
     if (c->spec_ids) (void)hipHostFree(c->spec_ids);
@@ -563,7 +574,7 @@ static int need_model(l3_ctx* c) {
 extern "C" int l3_reset_cache(l3_ctx* c) {
     CHECK_CTX(c);
     if (set_dev(c)) return 1;
-    for (auto& q : c->spec_q) c->spec_free.push_back(q.ev);  // the whole cache is cleared
+    for (auto& q : c->spec_q) c->spec_free.insert(c->spec_free.end(), {q.ev0, q.ev1, q.ev});  // cache cleared
     c->spec_q.clear();
     c->spec_base = c->spec_end = 0;
     c->dec_pos_mirror = -1;
@@ -978,8 +989,18 @@ static int spec_ahead(const l3_ctx* c) {
     return n >= l3_ctx::SPEC_AHEAD ? l3_ctx::SPEC_AHEAD : (int)n;
 }
 
+// replayed-step time: replaces the eager seed, then an EMA
 static void note_step_time(l3_ctx* c, double us) {
-    c->step_us = c->step_us > 0.0 ? 0.75 * c->step_us + 0.25 * us : us;
+    c->step_us = c->step_us > 0.0 && !c->step_us_seed ? 0.75 * c->step_us + 0.25 * us : us;
+    c->step_us_seed = false;
+}
+
+// the eager first decode step (per-kernel launches, id upload: an upper bound of a replayed
+// step) seeds step_us only while nothing better is known
+static void seed_step_time(l3_ctx* c, double us) {
+    if (c->step_us > 0.0) return;
+    c->step_us = us;
+    c->step_us_seed = true;
 }
 
 static double now_us() {
@@ -1082,18 +1103,22 @@ static int speculate(l3_ctx* c, int B) {
         // the time budget allows fewer than n
         const int k = n > 1 && limit - c->spec_end >= n ? n : 1;
         if (c->spec_end - c->spec_base + k > ahead) break;
+        hipEvent_t ev[3];
+        for (hipEvent_t& e : ev) {
+            if (c->spec_free.empty()) {
+                HIP_TRY(hipEventCreate(&e));
+            } else {
+                e = c->spec_free.back();
+                c->spec_free.pop_back();
+            }
+        }
+        HIP_TRY(hipEventRecord(ev[0], c->stream));
         HIP_TRY(hipGraphLaunch(k > 1 ? c->dec_exec_n : c->dec_exec, c->stream));
+        HIP_TRY(hipEventRecord(ev[1], c->stream));
         HIP_TRY(hipMemcpyAsync(c->spec_ids + (size_t)c->spec_end * B, c->spec_hist + (size_t)c->spec_end * B,
                                (size_t)k * B * 4, hipMemcpyDeviceToHost, c->stream));
-        hipEvent_t ev;
-        if (c->spec_free.empty()) {
-            HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        } else {
-            ev = c->spec_free.back();
-            c->spec_free.pop_back();
-        }
-        HIP_TRY(hipEventRecord(ev, c->stream));
-        c->spec_q.push_back({c->spec_end, k, ev, false});
+        HIP_TRY(hipEventRecord(ev[2], c->stream));
+        c->spec_q.push_back({c->spec_end, k, ev[0], ev[1], ev[2], false});
         c->spec_end += k;
     }
     return 0;
@@ -1115,7 +1140,7 @@ static int spec_resolve(l3_ctx* c) {
             HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
         }
     }
-    for (auto& q : c->spec_q) c->spec_free.push_back(q.ev);
+    for (auto& q : c->spec_q) c->spec_free.insert(c->spec_free.end(), {q.ev0, q.ev1, q.ev});
     c->spec_q.clear();
     c->spec_base = c->spec_end = 0;
     c->dec_pos_mirror = -1;
@@ -1144,10 +1169,13 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
             if (!q.done) {
                 HIP_TRY(hipEventSynchronize(q.ev));
                 q.done = true;
+                float ms = 0.f;  // the chunk's graph time on the device, per step
+                if (hipEventElapsedTime(&ms, q.ev0, q.ev1) == hipSuccess && ms > 0.f)
+                    note_step_time(c, 1e3 * (double)ms / q.n);
             }
             for (int i = 0; i < B; ++i) next_ids_host[i] = c->spec_ids[(size_t)start_pos * B + i];
             if (++c->spec_base == q.pos0 + q.n) {
-                c->spec_free.push_back(q.ev);
+                c->spec_free.insert(c->spec_free.end(), {q.ev0, q.ev1, q.ev});
                 c->spec_q.pop_front();
             }
             c->dec_last.assign(next_ids_host, next_ids_host + B);
@@ -1187,8 +1215,8 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
                                hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     // an eager decode step (per-kernel launches: an upper bound of the replayed step) seeds the
-    // run-ahead budget's step time; prefill calls (L > 1) do not
-    if (L == 1) note_step_time(c, now_us() - t_eager);
+    // run-ahead budget's step time until a replay is timed; prefill calls (L > 1) do not
+    if (L == 1) seed_step_time(c, now_us() - t_eager);
     for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
     // L3_DECODE_GRAPH=0 keeps every step eager (rocprofv3 kernel tracing does not survive
     // stream capture in this ROCm build)
@@ -1581,9 +1609,8 @@ extern "C" int l3_comm_unique_id(uint8_t id_out[128]) {
     return 0;
 }
 
-extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
-    CHECK_CTX(c);
-    if (set_dev(c)) return 1;
+// the comm stream / events a context's gathers use (before its communicator is set)
+static int comm_prepare(l3_ctx* c) {
     if (!c->comm_stream) {
         // high priority: a queue apart from the (normal-priority) forward streams, so the
         // transfer does not serialize behind the next forward's kernels in a shared HW queue
@@ -1595,11 +1622,73 @@ extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8
         HIP_TRY(hipEventCreateWithFlags(&c->comm_fwd_ev, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&c->comm_done_ev, hipEventDisableTiming));
     }
+    const int mode = env_knob("L3_COMM_MODE", 1);
+    c->comm_mode = mode == 0 || mode == 3 ? mode : 1;
+    return 0;
+}
+
+extern "C" int l3_comm_init(l3_ctx* c, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    CHECK_CTX(c);
+    if (set_dev(c) || comm_prepare(c)) return 1;
+    if (c->comm) return fail("l3_comm_init: communicator already initialised");
+    if (nranks < 1 || rank < 0 || rank >= nranks)
+        return fail("l3_comm_init: rank %d outside [0, %d)", rank, nranks);
     ncclUniqueId uid;
     memcpy(&uid, id, 128);
     NCCL_TRY(ncclCommInitRank(&c->comm, nranks, uid, rank));
     c->nranks = nranks;
     c->rank = rank;
+    return 0;
+}
+
+extern "C" int l3_comm_set_overlap(l3_ctx* c, int32_t on) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;  // joins a gather in flight: the new form applies from the next one
+    c->comm_mode = on ? 3 : 1;
+    return 0;
+}
+
+static int group_busids(l3_group* g, char* busids, int64_t cap);  // (below)
+
+// What RCCL itself reports for this rank (ncclCommCount / ncclCommUserRank / ncclCommCuDevice)
+// and every rank's PCI bus id, all-gathered over the communicator (collective: every rank calls
+// it), so a multi-GPU run can prove it ran N ranks on N distinct devices.
+extern "C" int l3_comm_info(l3_ctx* c, int32_t* nranks, int32_t* rank, int32_t* device, char* busids,
+                            int64_t busids_cap) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    char own[L3_BUSID_LEN] = {0};
+    HIP_TRY(hipDeviceGetPCIBusId(own, L3_BUSID_LEN - 1, c->device));
+    if (!c->comm) {
+        if (nranks) *nranks = 1;
+        if (rank) *rank = 0;
+        if (device) *device = c->device;
+        if (busids && busids_cap >= 1) memcpy(busids, own, L3_BUSID_LEN);
+        return 0;
+    }
+    int n = 0, r = 0, dev = -1;
+    NCCL_TRY(ncclCommCount(c->comm, &n));
+    NCCL_TRY(ncclCommUserRank(c->comm, &r));
+    NCCL_TRY(ncclCommCuDevice(c->comm, &dev));
+    if (nranks) *nranks = n;
+    if (rank) *rank = r;
+    if (device) *device = dev;
+    if (!busids) return 0;
+    if (c->group) return group_busids(c->group, busids, busids_cap);  // one process: no collective
+    if (busids_cap < n) return fail("l3_comm_info: room for %lld bus ids, the communicator has %d ranks",
+                                    (long long)busids_cap, n);
+    char* d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)n * L3_BUSID_LEN));
+    hipError_t e = hipMemcpyAsync(d + (size_t)r * L3_BUSID_LEN, own, L3_BUSID_LEN, hipMemcpyHostToDevice, c->stream);
+    ncclResult_t nr = e == hipSuccess ? ncclAllGather(d + (size_t)r * L3_BUSID_LEN, d, L3_BUSID_LEN, ncclChar,
+                                                      c->comm, c->stream)
+                                      : ncclSuccess;
+    if (e == hipSuccess && nr == ncclSuccess)
+        e = hipMemcpyAsync(busids, d, (size_t)n * L3_BUSID_LEN, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d);
+    if (nr != ncclSuccess) return fail("ncclAllGather(bus ids) failed: %s", ncclGetErrorString(nr));
+    if (e != hipSuccess) return fail("l3_comm_info copy failed: %s", hipGetErrorString(e));
     return 0;
 }
 
@@ -1619,24 +1708,26 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
                                      const int64_t* rows_per_rank, int32_t root) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_gather_logits: communicator not initialised");
+    if (c->group) return fail("l3_comm_gather_logits: this context is a member of an l3_group (use l3_group_*)");
     if (check_rows(c, "l3_comm_gather_logits", rows_per_rank, root)) return 1;
     if (c->rank == root && !dst_dev) return fail("l3_comm_gather_logits: null destination on the root");
     if (set_dev(c, false)) return 1;
     const int64_t VS = c->d.vocab_size;
-    // Mode 1: on the context stream, after the forward that wrote src and before the next one —
+    // Mode 1 (default): on the context stream, after the forward that wrote src and before the next one —
     // no cross-stream events, the transfer fully serialized.  The overlapped form (mode 0: the
     // transfer on the high-priority comm stream, ordered by events, the next lm_head waiting for
     // it) measured 7.96 ms/step against 6.94 at world 1 on MI355X, and 7.97 still with the
     // comm stream left empty (mode 2: root's own rows on the context stream) — the event
     // hand-offs between the streams, not the transfer, cost the step (profiles/r02_comm_modes.md).
     //
-    // Mode 3 (default): on the context stream as mode 1, but bracketed by events so that the
+    // Mode 3 (l3_comm_set_overlap): on the context stream as mode 1, but bracketed by events so that the
     // next l3_forward_dev's second batch part (aux stream) starts from the point before the
     // gather: its layers overlap the transfer, part 0 follows the gather on the context stream,
     // and both parts' lm_heads wait for its end (the rows it reads).  No comm stream; at world 1
     // (a self-copy) 6.038 / 6.051 ms/step against mode 1's 6.044 / 6.058, gathered rows
-    // bit-exact (profiles/r03_comm_mode3_ab.log)
-    static const int mode = env_knob("L3_COMM_MODE", 3);
+    // bit-exact (profiles/r03_comm_mode3_ab.log).  Not the default: at world 1 there is no
+    // transfer to overlap, and the overlap has not yet run against a real RCCL peer
+    const int mode = c->comm_mode;
     const bool on_ctx = mode == 1 || mode == 3;
     hipStream_t s = on_ctx ? c->stream : c->comm_stream;
     hipStream_t self_s = mode == 0 ? s : c->stream;
@@ -1682,6 +1773,7 @@ extern "C" int l3_comm_gather_argmax(l3_ctx* c, const float* src_dev, int32_t* d
                                      const int64_t* rows_per_rank, int32_t root) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_gather_argmax: communicator not initialised");
+    if (c->group) return fail("l3_comm_gather_argmax: this context is a member of an l3_group (use l3_group_*)");
     if (check_rows(c, "l3_comm_gather_argmax", rows_per_rank, root)) return 1;
     if (c->rank == root && !dst_dev) return fail("l3_comm_gather_argmax: null destination on the root");
     if (set_dev(c)) return 1;
@@ -1717,6 +1809,7 @@ extern "C" int l3_comm_gather_argmax(l3_ctx* c, const float* src_dev, int32_t* d
 extern "C" int l3_comm_allreduce_max(l3_ctx* c, double* value) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_allreduce_max: communicator not initialised");
+    if (c->group) return fail("l3_comm_allreduce_max: this context is a member of an l3_group (use l3_group_*)");
     if (set_dev(c)) return 1;
     double* d = nullptr;
     HIP_TRY(hipMalloc(&d, sizeof(double)));
@@ -1735,6 +1828,7 @@ extern "C" int l3_comm_allreduce_max(l3_ctx* c, double* value) {
 extern "C" int l3_comm_barrier(l3_ctx* c) {
     CHECK_CTX(c);
     if (!c->comm) return fail("l3_comm_barrier: communicator not initialised");
+    if (c->group) return fail("l3_comm_barrier: this context is a member of an l3_group (use l3_group_*)");
     if (set_dev(c)) return 1;
     float* one = nullptr;
     if (!c->scratch.empty()) one = (float*)c->scratch[0];
@@ -1745,5 +1839,275 @@ extern "C" int l3_comm_barrier(l3_ctx* c) {
     }
     NCCL_TRY(ncclAllReduce(one, one, 1, ncclFloat32, ncclSum, c->comm, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// One process driving the N GPUs of a node (SURVEY 8(b) l3_group_*): the
+// single-process drop-in of Llama.__call__ / generate (llama3.py:285-321).  One context per
+// device; communicators from ncclCommInitAll; a call uploads and launches every member's rows
+// without waiting (each member's work is asynchronous on its own streams), then one RCCL group
+// of point-to-point transfers brings the other members' rows to member 0, then one sync.
+// Batch row r is member r % n's local row r / n: the mapping does not depend on B, so a row's
+// KV cache stays on one device whatever batch sizes later calls use (the reference's cache row r
+// persists, llama3.py:138-153,184-187).
+struct l3_group {
+    int n = 0;
+    // the multi-member path (per-member launches, the grouped gather, the row interleave):
+    // n > 1, or n = 1 with L3_GROUP_MULTI_PATH=1 (tests: the 1-GPU box runs it against the
+    // single-device path); otherwise every call is member 0's own
+    bool multi = false;
+    std::vector<l3_ctx*> m;
+    std::vector<ncclComm_t> comms;
+    std::vector<int> devs;
+    l3_dims d{};                     // the model; max_batch_size the global batch
+    float* gbuf = nullptr;           // member 0: the other members' logits rows, member order
+    int64_t gbuf_rows = 0;
+    float* gout = nullptr;           // member 0: all rows in row order (host path)
+    int64_t gout_rows = 0;
+    int32_t* gids = nullptr;         // member 0: the other members' greedy ids
+    int64_t gids_n = 0;
+    std::vector<int64_t> tmp;        // host: one member's ids rows
+};
+
+static int group_rows(const l3_group* g, int B, int i) { return B > i ? (B - i + g->n - 1) / g->n : 0; }
+
+static int group_busids(l3_group* g, char* busids, int64_t cap) {
+    if (cap < g->n) return fail("l3_comm_info: room for %lld bus ids, the group has %d members", (long long)cap, g->n);
+    for (int i = 0; i < g->n; ++i) {
+        char b[L3_BUSID_LEN] = {0};
+        HIP_TRY(hipDeviceGetPCIBusId(b, L3_BUSID_LEN - 1, g->devs[(size_t)i]));
+        memcpy(busids + (size_t)i * L3_BUSID_LEN, b, L3_BUSID_LEN);
+    }
+    return 0;
+}
+
+extern "C" int l3_group_destroy(l3_group* g) {
+    if (!g) return 0;
+    for (l3_ctx* c : g->m)
+        if (c) { (void)hipSetDevice(c->device); (void)hipStreamSynchronize(c->stream); }
+    if (!g->m.empty() && g->m[0]) {
+        (void)hipSetDevice(g->m[0]->device);
+        dfree(g->gbuf); dfree(g->gout); dfree(g->gids);
+    }
+    for (size_t i = 0; i < g->comms.size(); ++i)
+        if (g->comms[i]) { (void)hipSetDevice(g->devs[i]); ncclCommDestroy(g->comms[i]); }
+    for (l3_ctx* c : g->m)
+        if (c) { c->comm = nullptr; c->group = nullptr; l3_destroy(c); }
+    delete g;
+    return 0;
+}
+
+extern "C" int l3_group_create(int32_t ndev, const int32_t* devices, const l3_dims* dims, l3_group** out) {
+    if (!devices || !dims || !out) return fail("l3_group_create: null argument");
+    int have = 0;
+    HIP_TRY(hipGetDeviceCount(&have));
+    if (ndev < 1 || ndev > have) return fail("l3_group_create: %d devices requested, %d present", ndev, have);
+    for (int i = 0; i < ndev; ++i) {
+        if (devices[i] < 0 || devices[i] >= have) return fail("l3_group_create: no device %d", devices[i]);
+        for (int j = 0; j < i; ++j)
+            if (devices[j] == devices[i]) return fail("l3_group_create: device %d listed twice", devices[i]);
+    }
+    if (dims->max_batch_size < 1) return fail("l3_group_create: max_batch_size %d < 1", dims->max_batch_size);
+    l3_group* g = new l3_group();
+    g->n = ndev;
+    g->d = *dims;
+    g->devs.assign(devices, devices + ndev);
+    g->multi = ndev > 1 || env_knob("L3_GROUP_MULTI_PATH", 0) != 0;
+    l3_dims local = *dims;  // each member holds the KV cache of its rows only
+    local.max_batch_size = (dims->max_batch_size + ndev - 1) / ndev;
+    g->m.assign((size_t)ndev, nullptr);
+    for (int i = 0; i < ndev; ++i)
+        if (l3_create(devices[i], &local, &g->m[(size_t)i])) {
+            const std::string e = g_err;
+            l3_group_destroy(g);
+            return fail("l3_group_create: member %d (device %d): %s", i, devices[i], e.c_str());
+        }
+    g->comms.assign((size_t)ndev, nullptr);
+    const ncclResult_t r = ncclCommInitAll(g->comms.data(), ndev, g->devs.data());
+    if (r != ncclSuccess) {
+        g->comms.assign((size_t)ndev, nullptr);
+        l3_group_destroy(g);
+        return fail("ncclCommInitAll over %d devices failed: %s", ndev, ncclGetErrorString(r));
+    }
+    for (int i = 0; i < ndev; ++i) {
+        l3_ctx* c = g->m[(size_t)i];
+        if (set_dev(c) || comm_prepare(c)) { const std::string e = g_err; l3_group_destroy(g); return fail("%s", e.c_str()); }
+        c->comm = g->comms[(size_t)i];
+        c->comm_owned = false;
+        c->group = g;
+        c->nranks = ndev;
+        c->rank = i;
+        c->comm_mode = 1;  // the group's gathers are always serialized on the member streams
+    }
+    *out = g;
+    return 0;
+}
+
+extern "C" int l3_group_context(l3_group* g, int32_t i, l3_ctx** ctx) {
+    if (!g || !ctx) return fail("l3_group_context: null argument");
+    if (i < 0 || i >= g->n) return fail("l3_group_context: member %d outside [0, %d)", i, g->n);
+    *ctx = g->m[(size_t)i];
+    return 0;
+}
+
+extern "C" int l3_group_upload_weight(l3_group* g, int32_t layer, int32_t kind, const float* host,
+                                      int64_t rows, int64_t cols) {
+    if (!g) return fail("null group");
+    for (l3_ctx* c : g->m)
+        if (l3_upload_weight(c, layer, kind, host, rows, cols)) return 1;
+    return 0;
+}
+
+extern "C" int l3_group_finalize(l3_group* g) {
+    if (!g) return fail("null group");
+    for (l3_ctx* c : g->m)
+        if (l3_finalize(c)) return 1;
+    return 0;
+}
+
+extern "C" int l3_group_synchronize(l3_group* g) {
+    if (!g) return fail("null group");
+    for (l3_ctx* c : g->m)
+        if (l3_synchronize(c)) return 1;
+    return 0;
+}
+
+// every member with rows: checks (all before any launch), then ids (host rows r = i + n*j, or
+// the member's device block) and its forward into its own logits workspace, launched without
+// waiting; each member's decode state is left (no graph replays in a multi-member call)
+static int group_launch(l3_group* g, const int64_t* ids_host, const int32_t* const* ids_dev, int B, int L,
+                        int start_pos) {
+    if (B > g->d.max_batch_size) return fail("batch %d exceeds max_batch_size %d", B, g->d.max_batch_size);
+    if (B <= 0 || L <= 0) return fail("empty input: B=%d L=%d", B, L);
+    for (int i = 0; i < g->n; ++i) {
+        const int nb = group_rows(g, B, i);
+        l3_ctx* c = g->m[(size_t)i];
+        if (!nb) continue;
+        if (need_model(c) || check_call(c, nb, L, start_pos) || set_dev(c) || spec_resolve(c) || ensure_ws(c, nb, L))
+            return 1;
+        c->dec_pos_mirror = -1;
+    }
+    for (int i = 0; i < g->n; ++i) {
+        const int nb = group_rows(g, B, i);
+        l3_ctx* c = g->m[(size_t)i];
+        if (!nb) continue;
+        if (set_dev(c)) return 1;
+        const int32_t* ids = ids_dev ? ids_dev[i] : c->ids;
+        if (ids_host) {
+            g->tmp.resize((size_t)nb * L);
+            for (int j = 0; j < nb; ++j)
+                memcpy(&g->tmp[(size_t)j * L], ids_host + ((int64_t)i + (int64_t)g->n * j) * L, (size_t)L * 8);
+            if (upload_ids(c, g->tmp.data(), (int64_t)nb * L)) return 1;
+        }
+        if (forward_dev(c, ids, nb, L, start_pos, c->logits)) return 1;
+    }
+    return 0;
+}
+
+// rows of `each` floats per row: member i's nb_i rows (src_i) to member 0, interleaved into
+// dst [B, each] in row order (row i + n*j <- member i's row j).  src_0 goes straight into dst.
+template <typename T>
+static int group_gather(l3_group* g, int B, int64_t each, T** src, T* peer_buf, T* dst, ncclDataType_t type) {
+    l3_ctx* c0 = g->m[0];
+    NCCL_TRY(ncclGroupStart());
+    int64_t off = 0;
+    for (int i = 1; i < g->n; ++i) {
+        const int64_t nb = group_rows(g, B, i);
+        if (!nb) continue;
+        ncclResult_t r = ncclRecv(peer_buf + off * each, (size_t)(nb * each), type, i, g->comms[0], c0->stream);
+        if (r == ncclSuccess)
+            r = ncclSend(src[i], (size_t)(nb * each), type, 0, g->comms[(size_t)i], g->m[(size_t)i]->stream);
+        if (r != ncclSuccess) {
+            (void)ncclGroupEnd();
+            return fail("group gather (member %d): %s", i, ncclGetErrorString(r));
+        }
+        off += nb;
+    }
+    NCCL_TRY(ncclGroupEnd());
+    HIP_TRY(hipSetDevice(c0->device));
+    const size_t pitch = (size_t)g->n * each * sizeof(T), w = (size_t)each * sizeof(T);
+    HIP_TRY(hipMemcpy2DAsync(dst, pitch, src[0], w, w, (size_t)group_rows(g, B, 0), hipMemcpyDeviceToDevice,
+                             c0->stream));
+    off = 0;
+    for (int i = 1; i < g->n; ++i) {
+        const int64_t nb = group_rows(g, B, i);
+        if (!nb) continue;
+        HIP_TRY(hipMemcpy2DAsync(dst + (size_t)i * each, pitch, peer_buf + off * each, w, w, (size_t)nb,
+                                 hipMemcpyDeviceToDevice, c0->stream));
+        off += nb;
+    }
+    return 0;
+}
+
+// member-0 buffer of at least `rows` rows of `each` elements (grown; the stream is idle when
+// it grows: callers grow before launching)
+template <typename T>
+static int group_buf(l3_group* g, T** p, int64_t* have, int64_t rows, int64_t each) {
+    if (rows <= *have) return 0;
+    HIP_TRY(hipSetDevice(g->m[0]->device));
+    HIP_TRY(hipStreamSynchronize(g->m[0]->stream));
+    dfree(*p);
+    *p = nullptr;
+    *have = 0;
+    HIP_TRY(hipMalloc(p, (size_t)rows * each * sizeof(T)));
+    *have = rows;
+    return 0;
+}
+
+extern "C" int l3_group_forward_dev(l3_group* g, const int32_t* const* ids_dev, int32_t B, int32_t L,
+                                    int32_t start_pos, float* logits_dev) {
+    if (!g || !ids_dev || !logits_dev) return fail("l3_group_forward_dev: null argument");
+    if (!g->multi || B == 1) return l3_forward_dev(g->m[0], ids_dev[0], B, L, start_pos, logits_dev);
+    const int64_t VS = g->d.vocab_size;
+    if (group_buf(g, &g->gbuf, &g->gbuf_rows, B - group_rows(g, B, 0), VS)) return 1;
+    if (group_launch(g, nullptr, ids_dev, B, L, start_pos)) return 1;
+    std::vector<float*> src((size_t)g->n);
+    for (int i = 0; i < g->n; ++i) src[(size_t)i] = g->m[(size_t)i]->logits;
+    return group_gather(g, B, VS, src.data(), g->gbuf, logits_dev, ncclFloat32);
+}
+
+extern "C" int l3_group_forward_host(l3_group* g, const int64_t* ids_host, int32_t B, int32_t L,
+                                     int32_t start_pos, float* logits_host) {
+    if (!g || !ids_host || !logits_host) return fail("l3_group_forward_host: null argument");
+    // rows on member 0 only: its own single-device host path (pinned per-part copies)
+    if (!g->multi || B == 1) return l3_forward_host(g->m[0], ids_host, B, L, start_pos, logits_host);
+    const int64_t VS = g->d.vocab_size;
+    if (group_buf(g, &g->gbuf, &g->gbuf_rows, B - group_rows(g, B, 0), VS) ||
+        group_buf(g, &g->gout, &g->gout_rows, B, VS))
+        return 1;
+    if (group_launch(g, ids_host, nullptr, B, L, start_pos)) return 1;
+    std::vector<float*> src((size_t)g->n);
+    for (int i = 0; i < g->n; ++i) src[(size_t)i] = g->m[(size_t)i]->logits;
+    if (group_gather(g, B, VS, src.data(), g->gbuf, g->gout, ncclFloat32)) return 1;
+    l3_ctx* c0 = g->m[0];
+    HIP_TRY(hipMemcpyAsync(logits_host, g->gout, (size_t)B * VS * 4, hipMemcpyDeviceToHost, c0->stream));
+    return l3_group_synchronize(g);
+}
+
+extern "C" int l3_group_greedy_step_host(l3_group* g, const int64_t* ids_host, int32_t B, int32_t L,
+                                         int32_t start_pos, int64_t* next_ids_host) {
+    if (!g || !ids_host || !next_ids_host) return fail("l3_group_greedy_step_host: null argument");
+    // single-prompt greedy decode stays on one GPU (member 0: graph-replayed steps, run-ahead)
+    if (!g->multi || B == 1) return l3_greedy_step_host(g->m[0], ids_host, B, L, start_pos, next_ids_host, nullptr);
+    // gids: [0, B) the ids in row order, [B, 2B) the other members' ids as received
+    if (group_buf(g, &g->gids, &g->gids_n, 2 * (int64_t)B, 1)) return 1;
+    if (group_launch(g, ids_host, nullptr, B, L, start_pos)) return 1;
+    std::vector<int32_t*> src((size_t)g->n);
+    for (int i = 0; i < g->n; ++i) {
+        l3_ctx* c = g->m[(size_t)i];
+        const int nb = group_rows(g, B, i);
+        src[(size_t)i] = c->amax;
+        if (!nb) continue;
+        if (set_dev(c)) return 1;
+        // np.argmax over the member's rows (llama3.py:320: first index on ties)
+        if (timed(c, L3_K_ARGMAX, [&] { return launch_argmax(c->logits, nb, (int)c->d.vocab_size, c->amax, c->stream); }))
+            return 1;
+    }
+    if (group_gather(g, B, 1, src.data(), g->gids + B, g->gids, ncclInt32)) return 1;
+    std::vector<int32_t> ids32((size_t)B);
+    HIP_TRY(hipMemcpyAsync(ids32.data(), g->gids, (size_t)B * 4, hipMemcpyDeviceToHost, g->m[0]->stream));
+    if (l3_group_synchronize(g)) return 1;
+    for (int b = 0; b < B; ++b) next_ids_host[b] = ids32[(size_t)b];
     return 0;
 }

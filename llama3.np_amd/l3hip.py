@@ -86,7 +86,20 @@ _SIGNATURES = {
     "l3_comm_gather_argmax": (ctypes.c_int, [_P, _P, _P, _P, _I32]),
     "l3_comm_barrier": (ctypes.c_int, [_P]),
     "l3_comm_allreduce_max": (ctypes.c_int, [_P, _P]),
+    "l3_comm_info": (ctypes.c_int, [_P, _P, _P, _P, _P, _I64]),
+    "l3_comm_set_overlap": (ctypes.c_int, [_P, _I32]),
+    "l3_group_create": (ctypes.c_int, [_I32, _P, _P, _P]),
+    "l3_group_destroy": (ctypes.c_int, [_P]),
+    "l3_group_context": (ctypes.c_int, [_P, _I32, _P]),
+    "l3_group_upload_weight": (ctypes.c_int, [_P, _I32, _I32, _P, _I64, _I64]),
+    "l3_group_finalize": (ctypes.c_int, [_P]),
+    "l3_group_forward_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
+    "l3_group_forward_dev": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
+    "l3_group_greedy_step_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
+    "l3_group_synchronize": (ctypes.c_int, [_P]),
 }
+
+BUSID_LEN = 16  # L3_BUSID_LEN
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -229,15 +242,24 @@ class Context:
         check(lib().l3_create(device, ctypes.byref(dims), ctypes.byref(self._h)))
         self.dims = dims
         self.device = device
+        self._owned = True
+
+    @classmethod
+    def _member(cls, handle: ctypes.c_void_p, dims: Dims, device: int, group) -> "Context":
+        """A group member's context: owned by the group (never destroyed through this object,
+        which keeps the group alive)."""
+        c = cls.__new__(cls)
+        c._h, c.dims, c.device, c._owned, c._group = handle, dims, device, False, group
+        return c
 
     @property
     def handle(self):
         return self._h
 
     def close(self):
-        if self._h:
+        if self._h and getattr(self, "_owned", True):
             lib().l3_destroy(self._h)
-            self._h = ctypes.c_void_p()
+        self._h = ctypes.c_void_p()
 
     def __del__(self):
         try:
@@ -378,6 +400,26 @@ class Context:
         rows = self._rows(rows_per_rank)
         check(lib().l3_comm_gather_argmax(self._h, src_dev, dst_dev or 0, ptr(rows), root))
 
+    def comm_info(self, gather_busids: bool = True) -> dict:
+        """What RCCL reports for this rank (ncclCommCount / ncclCommUserRank /
+        ncclCommCuDevice) and, with ``gather_busids`` (collective: every rank calls it), every
+        rank's PCI bus id in rank order."""
+        n, r, d = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_int32(0)
+        cap = getattr(self, "nranks", 1) if gather_busids else 0
+        buf = ctypes.create_string_buffer(BUSID_LEN * max(cap, 1))
+        check(lib().l3_comm_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(d),
+                                 buf if gather_busids else None, cap))
+        out = {"nranks": n.value, "rank": r.value, "device": d.value}
+        if gather_busids:
+            raw = buf.raw
+            out["busids"] = [raw[i * BUSID_LEN:(i + 1) * BUSID_LEN].split(b"\0")[0].decode()
+                             for i in range(n.value)]
+        return out
+
+    def set_comm_overlap(self, on: bool) -> None:
+        """The overlapped logits gather (next forward's second batch part runs during it)."""
+        check(lib().l3_comm_set_overlap(self._h, int(bool(on))))
+
     def comm_barrier(self) -> None:
         check(lib().l3_comm_barrier(self._h))
 
@@ -443,6 +485,104 @@ class Context:
         check(lib().l3_op_ffn_host(self._h, ptr(x), x.size // D, D, FD, ptr(wg), ptr(wu), ptr(wd),
                                    ptr(y)))
         return y
+
+
+def member_rows(B: int, n: int, i: int) -> int:
+    """Rows of group member i (of n) in a batch of B: global rows i, i + n, i + 2n, ... — the
+    l3_group row mapping (row r on member r % n as its local row r // n), which does not depend
+    on B, so a row's KV cache stays on one device across calls of any batch size."""
+    if n <= 0 or not 0 <= i < n:
+        raise ValueError(f"bad member {i} of {n}")
+    return (B - i + n - 1) // n if B > i else 0
+
+
+class Group:
+    """One process driving ``devices`` (l3_group_*, include/llama3hip.h): one context per
+    device, RCCL communicators from ncclCommInitAll, batch row r on member r % n (its local
+    row r // n).  Same upload / finalize / forward / greedy_step surface as ``Context``."""
+
+    def __init__(self, dims: Dims, devices):
+        devs = np.ascontiguousarray(list(devices), dtype=np.int32)
+        if devs.ndim != 1 or devs.size == 0:
+            raise ValueError("devices must be a non-empty list of device ordinals")
+        self._h = ctypes.c_void_p()
+        check(lib().l3_group_create(int(devs.size), ptr(devs), ctypes.byref(dims), ctypes.byref(self._h)))
+        self.dims = dims
+        self.devices = [int(x) for x in devs]
+        self.n = len(self.devices)
+        local = Dims.from_buffer_copy(dims)
+        local.max_batch_size = -(-dims.max_batch_size // self.n)
+        self.members = []
+        for i, dv in enumerate(self.devices):
+            h = ctypes.c_void_p()
+            check(lib().l3_group_context(self._h, i, ctypes.byref(h)))
+            m = Context._member(h, local, dv, self)
+            m.nranks, m.rank = self.n, i  # its communicator (ncclCommInitAll), used via the group
+            self.members.append(m)
+
+    def close(self):
+        if self._h:
+            for m in self.members:
+                m._h = ctypes.c_void_p()
+            lib().l3_group_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def rows(self, B: int, i: int) -> int:
+        """Rows of member i in a batch of B (rows i, i + n, ...)."""
+        return member_rows(B, self.n, i)
+
+    def upload(self, layer: int, kind: int, w: np.ndarray) -> None:
+        a = np.ascontiguousarray(w, dtype=np.float32)
+        rows, cols = (1, a.shape[0]) if a.ndim == 1 else a.shape
+        check(lib().l3_group_upload_weight(self._h, layer, kind, ptr(a), rows, cols))
+
+    def finalize(self) -> None:
+        check(lib().l3_group_finalize(self._h))
+
+    def forward(self, ids: np.ndarray, start_pos: int) -> np.ndarray:
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        B, L = ids.shape
+        out = pinned.empty((B, self.dims.vocab_size), np.float32)
+        check(lib().l3_group_forward_host(self._h, ptr(ids), B, L, start_pos, ptr(out)))
+        return out
+
+    def forward_dev(self, ids_dev, B: int, L: int, start_pos: int, logits_dev: int) -> None:
+        """ids_dev: one device pointer per member (its rows, int32); logits_dev on member 0."""
+        arr = (ctypes.c_void_p * self.n)(*[ctypes.c_void_p(p or 0) for p in ids_dev])
+        check(lib().l3_group_forward_dev(self._h, arr, B, L, start_pos, logits_dev))
+
+    def greedy_step(self, ids: np.ndarray, start_pos: int, want_logits: bool = False):
+        if want_logits:
+            raise NotImplementedError("Group.greedy_step returns ids only")
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        B, L = ids.shape
+        nxt = np.empty(B, np.int64)
+        check(lib().l3_group_greedy_step_host(self._h, ptr(ids), B, L, start_pos, ptr(nxt)))
+        return nxt, None
+
+    def set_decode_horizon(self, end_pos: int) -> None:
+        self.members[0].set_decode_horizon(end_pos)
+
+    def synchronize(self) -> None:
+        check(lib().l3_group_synchronize(self._h))
+
+    def _single(self) -> Context:
+        if self.n != 1:
+            raise RuntimeError("a per-block call on a multi-device Llama: its KV cache rows are spread "
+                               "over the devices; build a TransformerBlock from the weights instead")
+        return self.members[0]
+
+    def layer_forward(self, layer: int, x: np.ndarray, start_pos: int) -> np.ndarray:
+        return self._single().layer_forward(layer, x, start_pos)
+
+    def attention_forward(self, layer: int, x: np.ndarray, start_pos: int) -> np.ndarray:
+        return self._single().attention_forward(layer, x, start_pos)
 
 
 def launch_key() -> str:

@@ -35,7 +35,7 @@ import os
 import sys
 import time
 import zipfile
-from typing import Iterator, Mapping, Optional
+from typing import Iterator, Mapping, Optional, Sequence
 
 import numpy as np
 
@@ -268,8 +268,15 @@ class Llama:
     ``generate`` runs argmax on the device and copies back only ids."""
 
     def __init__(self, model_path: str, args: ModelArgs, device: Optional[int] = None,
-                 keep_host_weights: bool = True):
-        """``device`` / ``keep_host_weights`` are extensions.  With
+                 keep_host_weights: bool = True, devices: Optional[Sequence[int]] = None):
+        """``device`` / ``keep_host_weights`` / ``devices`` are extensions.
+
+        ``devices=[0, ..., N-1]``: one process drives N GPUs (``l3hip.Group``, the C ABI's
+        l3_group_*).  Every call keeps the reference's signature and result: batch row r runs on
+        ``devices[r % N]`` (rows never interact, llama3.py:163-211), the other devices' logits
+        rows reach the first device in one RCCL gather over xGMI, and ``__call__`` returns the
+        full ``[B, 1, VS]``; a single prompt (B = 1) runs on the first device alone, greedy
+        decode included.  Only the constructor changes for a reference user.  With
         ``keep_host_weights=False`` every ``.npz`` member is read, uploaded to HBM and
         dropped before the next is read (NumPy's NpzFile reads members lazily), so host
         memory peaks at one tensor instead of the whole checkpoint (32 GB for the
@@ -298,35 +305,51 @@ class Llama:
         self.freqs_cos, self.freqs_sin = compute_cos_sin_cache(args.dim // args.n_heads,
                                                                args.max_seq_len)
         hidden = weight.get("model.layers.0.mlp.gate_proj.weight").shape[0]
-        dev = DEFAULT_DEVICE if device is None else device
-        self._ctx = l3hip.Context(_dims(args, hidden, args.n_layers, args.vocab_size), dev)
+        dims = _dims(args, hidden, args.n_layers, args.vocab_size)
+        if devices is not None:
+            if device is not None:
+                raise ValueError("pass device or devices, not both")
+            self._group = l3hip.Group(dims, devices)
+            self._ctx = self._group.members[0]
+            tgt = self._group  # uploads go to every device; calls shard the batch rows
+        else:
+            self._group = None
+            self._ctx = l3hip.Context(dims, DEFAULT_DEVICE if device is None else device)
+            tgt = self._ctx
+        self._target = tgt
         emb = weight.get("model.embed_tokens.weight")
-        self._ctx.upload(0, l3hip.W_EMBED, emb)
+        tgt.upload(0, l3hip.W_EMBED, emb)
         self.tok_embedding = emb if keep else _Dropped(emb.shape)
         del emb
-        self.layers = [TransformerBlock(weight, i, args, _bind=(self._ctx, i), _keep_host=keep)
+        self.layers = [TransformerBlock(weight, i, args, _bind=(tgt, i), _keep_host=keep)
                        for i in range(args.n_layers)]
         norm_w = weight.get("model.norm.weight")
         self.norm = RMSNorm(norm_w if keep else np.array(norm_w), eps=args.norm_eps)
-        self._ctx.upload(0, l3hip.W_FINAL_NORM, norm_w)
+        tgt.upload(0, l3hip.W_FINAL_NORM, norm_w)
         lm = weight.get("lm_head.weight")
-        self._ctx.upload(0, l3hip.W_LM_HEAD, lm)
+        tgt.upload(0, l3hip.W_LM_HEAD, lm)
         self.lm_head_weight = lm.T if keep else _Dropped(lm.shape[::-1])
         del lm
-        self._ctx.finalize()
+        tgt.finalize()
         del weight, norm_w
         if pool is not None:
             pool.clear()
 
     @property
     def context(self) -> l3hip.Context:
+        """The device context (with ``devices=``: the first device's member context)."""
         return self._ctx
+
+    @property
+    def group(self) -> Optional[l3hip.Group]:
+        """The multi-device group (``devices=``), else None."""
+        return self._group
 
     def __call__(self, input_ids, start_pos: int):
         ids = np.asarray(input_ids)
         if ids.ndim != 2:
             raise ValueError(f"input_ids must be [B, L], got shape {ids.shape}")
-        logits = self._ctx.forward(ids, int(start_pos))
+        logits = self._target.forward(ids, int(start_pos))
         return logits[:, None, :]
 
     def generate(self, input_ids, max_new_tokens: int) -> Iterator[np.ndarray]:
@@ -337,13 +360,13 @@ class Llama:
         max_new_tokens), and a schedule left early is undone before any later call."""
         ids = np.asarray(input_ids)
         _, L = ids.shape
-        self._ctx.set_decode_horizon(max_new_tokens)
+        self._target.set_decode_horizon(max_new_tokens)
         next_id = None
         for i, curr_pos in enumerate(range(L, max_new_tokens)):
             if i == 0:
-                nxt, _ = self._ctx.greedy_step(ids, 0)
+                nxt, _ = self._target.greedy_step(ids, 0)
             else:
-                nxt, _ = self._ctx.greedy_step(next_id, curr_pos)
+                nxt, _ = self._target.greedy_step(next_id, curr_pos)
             next_id = nxt.reshape(-1, 1)
             yield next_id
 
@@ -352,8 +375,22 @@ class Llama:
         same schedule, same decode hole — computed as one device-side loop of
         graph-replayed steps with a single copy-back.  Returns int64
         ``[B, max_new_tokens - L]``.  Unlike ``generate`` it is not lazy: every step
-        runs, so use it when the caller consumes all tokens."""
-        return self._ctx.greedy_generate(np.asarray(input_ids), max_new_tokens)
+        runs, so use it when the caller consumes all tokens.  On a multi-device model a batch of
+        more than one row steps through ``Group.greedy_step`` (each device its rows, the ids
+        gathered) instead of the single-device graph loop."""
+        ids = np.asarray(input_ids)
+        if self._group is None or self._group.n == 1 or ids.shape[0] == 1:
+            return self._ctx.greedy_generate(ids, max_new_tokens)
+        B, L = ids.shape
+        if max_new_tokens > self.args.max_seq_len:
+            raise RuntimeError(f"generate: last decode position {max_new_tokens - 1} exceeds "
+                               f"max_seq_len {self.args.max_seq_len}")
+        out = np.empty((B, max(0, max_new_tokens - L)), np.int64)
+        nxt = None
+        for i, pos in enumerate(range(L, max_new_tokens)):
+            nxt, _ = self._group.greedy_step(ids if i == 0 else nxt.reshape(-1, 1), 0 if i == 0 else pos)
+            out[:, i] = nxt
+        return out
 
 
 def main(argv=None, tokenizer_path="./tokenizer.model.np", model_path="./stories15M.model.npz"):

@@ -36,7 +36,7 @@ sys.exit(rc if r == fail_rank else 0)
 """
 
 
-def _run(tmp_path, n, fail_rank=-1, rc=0, sleep_rank=-1, grace_s=20.0):
+def _run(tmp_path, n, fail_rank=-1, rc=0, sleep_rank=-1, grace_s=20.0, timeout_s=120):
     stub = tmp_path / "stub.py"
     stub.write_text(STUB)
     out = tmp_path / "out"
@@ -44,7 +44,7 @@ def _run(tmp_path, n, fail_rank=-1, rc=0, sleep_rank=-1, grace_s=20.0):
     log = tmp_path / "stdout.txt"
     with open(log, "w") as f:
         status = bench.spawn_ranks(n, [str(out), str(fail_rank), str(rc), str(sleep_rank)],
-                                   cmd=[sys.executable, str(stub)], timeout_s=120, grace_s=grace_s,
+                                   cmd=[sys.executable, str(stub)], timeout_s=timeout_s, grace_s=grace_s,
                                    out=f)
     envs = {}
     for p in out.iterdir():
@@ -98,6 +98,17 @@ def test_spawn_kills_peers_of_a_failed_rank(tmp_path):
     # after the grace period and reports rank 1's status
     status, envs, _ = _run(tmp_path, 3, fail_rank=1, rc=5, sleep_rank=2, grace_s=1.0)
     assert status == 5 and sorted(envs) == [0, 1, 2]
+
+
+def test_spawn_timeout_kills_hung_launch(tmp_path):
+    # no rank fails but one never returns (every rank stuck in RCCL init looks like this): the
+    # launch-wide timeout kills it and reports 124; the finally reaps every child
+    import time
+
+    t0 = time.time()
+    status, envs, _ = _run(tmp_path, 2, sleep_rank=1, timeout_s=2.0)
+    assert status == 124 and sorted(envs) == [0, 1]
+    assert time.time() - t0 < 60
 
 
 def test_bench_cli_spawns_without_world_size(tmp_path):

@@ -331,12 +331,14 @@ def test_sharded_prefill_world1_rccl(tmpdir_mod):
     np.testing.assert_array_equal(nxt[:, 0], np.argmax(want[:, 0, :], axis=-1))
 
 
-def test_gather_pipelined_forwards_world1(tmpdir_mod):
-    """Forwards and gathers queued back to back on one logits buffer, as bench.py does: the
-    next forward's second batch part starts before the gather ends (overlapping it), part 0
-    and every lm_head wait for it.  Three forwards, two gathers into separate roots, then D2H — each
-    holds its own step's logits, bit-identical to Llama.__call__ on the same rows, under each
-    batch split."""
+@pytest.mark.parametrize("overlap", [False, True])
+def test_gather_pipelined_forwards_world1(tmpdir_mod, overlap):
+    """Forwards and gathers queued back to back on one logits buffer, as bench.py does — the
+    gather serialized on the context stream (default) or overlapped (l3_comm_set_overlap: the
+    next forward's second batch part starts before the gather ends, part 0 and every lm_head
+    wait for it).  Three forwards, two gathers into separate roots, then D2H — each holds its
+    own step's logits, bit-identical to Llama.__call__ on the same rows, under each batch
+    split."""
     args = synth.stories15m(16)
     _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
     VS, B, L = args.vocab_size, 16, 64
@@ -347,6 +349,7 @@ def test_gather_pipelined_forwards_world1(tmpdir_mod):
     m = llama3.Llama(path, args)
     ctx = m.context
     ctx.comm_init(1, 0, l3hip.comm_unique_id())
+    ctx.set_comm_overlap(overlap)
     ids_dev = [ctx.alloc(x.nbytes) for x in ids]
     for d, x in zip(ids_dev, ids):
         ctx.h2d(d, x)
@@ -372,10 +375,11 @@ def test_gather_pipelined_forwards_world1(tmpdir_mod):
 
 
 def test_gather_overlap_entry_points_world1(tmpdir_mod):
-    """The gather's overlap with the next forward's second batch part (L3_COMM_MODE 3) is taken
-    only by l3_forward_dev right after a gather: a host forward, a forward of another batch size
-    (workspace regrowth) and a forward after a decode step all see the gathered rows and the
-    logits of their own step, bit-identical to Llama.__call__."""
+    """The gather's overlap with the next forward's second batch part (l3_comm_set_overlap) is
+    taken only by l3_forward_dev right after a gather: a host forward, a forward of another batch
+    size (workspace regrowth) and a forward after a greedy decode step (which clears the overlap
+    through l3_greedy_step_host) all see the gathered rows and the logits of their own step,
+    bit-identical to Llama.__call__."""
     args = synth.stories15m(24)
     _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
     VS, L = args.vocab_size, 48
@@ -387,6 +391,7 @@ def test_gather_overlap_entry_points_world1(tmpdir_mod):
     ctx = m.context
     ctx.set_batch_split(2, min_tokens=1)
     ctx.comm_init(1, 0, l3hip.comm_unique_id())
+    ctx.set_comm_overlap(True)
     ids_dev = [ctx.alloc(x.nbytes) for x in ids]
     for d, x in zip(ids_dev, ids):
         ctx.h2d(d, x)
@@ -411,7 +416,37 @@ def test_gather_overlap_entry_points_world1(tmpdir_mod):
         ctx.gather_logits(buf, dst[k % 2], [16], root=0)
     for k in range(2):
         np.testing.assert_array_equal(ctx.d2h(np.empty((16, VS), np.float32), dst[k]), want[k])
+    # gather -> a greedy decode step on other rows (a cache-reading entry point: joins the gather,
+    # may arm a captured step and queue run-ahead steps) -> forward_dev -> gather: the decode
+    # step's ids are the reference's, and the next forward's rows and gathered rows are exact
+    ref2 = llama3.Llama(path, args)
+    ref2(ids[0], 0)
+    tok = ref2(ids[0][:, -1:], L)[:, 0, :].argmax(-1)
+    ctx.forward_dev(ids_dev[0], 16, L, 0, buf)
+    ctx.gather_logits(buf, dst[0], [16], root=0)
+    nxt, _ = ctx.greedy_step(ids[0][:, -1:].astype(np.int64), L)
+    np.testing.assert_array_equal(nxt, tok)
+    ctx.forward_dev(ids_dev[1], 16, L, 0, buf)
+    ctx.gather_logits(buf, dst[1], [16], root=0)
+    np.testing.assert_array_equal(ctx.d2h(np.empty((16, VS), np.float32), dst[0]), want[0])
+    np.testing.assert_array_equal(ctx.d2h(np.empty((16, VS), np.float32), dst[1]), want[1])
+    np.testing.assert_array_equal(ctx.d2h(np.empty((16, VS), np.float32), buf), want[1])
     ctx.set_batch_split(2)
+
+
+def test_comm_info_world1(tmpdir_mod):
+    """l3_comm_info: without a communicator one rank on this device; after l3_comm_init at
+    world 1 RCCL's own count / rank / device and the bus id gathered over RCCL (what the N > 1
+    bench line reports: rccl_nranks and devices)."""
+    args = synth.stories15m(2)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    ctx = llama3.Llama(path, args).context
+    alone = ctx.comm_info(gather_busids=False)
+    assert alone == {"nranks": 1, "rank": 0, "device": 0}
+    ctx.comm_init(1, 0, l3hip.comm_unique_id())
+    info = ctx.comm_info()
+    assert info["nranks"] == 1 and info["rank"] == 0 and info["device"] == 0
+    assert len(info["busids"]) == 1 and info["busids"][0].count(":") == 2, info
 
 
 # ---- decode state / graph replay ------------------------------------------------------------
@@ -829,6 +864,17 @@ def test_c4_full_batch_2048_one_gpu(tmpdir_mod):
     m2 = llama3.Llama(path, args)
     sp = ShardedPrefill.on_device(m2, 1, 0, bcast_uid=lambda uid: uid)
     np.testing.assert_array_equal(sp(ids, 0), full)
+    del m2, sp
+    # the single-process drop-in (Llama(devices=...), l3_group_*) at N = 1: bit-identical, also
+    # through the multi-member path (per-member launch, grouped gather, row interleave)
+    for multi in ("0", "1"):
+        os.environ["L3_GROUP_MULTI_PATH"] = multi
+        try:
+            mg = llama3.Llama(path, args, devices=[0])
+        finally:
+            os.environ.pop("L3_GROUP_MULTI_PATH", None)
+        np.testing.assert_array_equal(mg(ids, 0), full)
+        del mg
 
 
 @pytest.mark.parametrize("M", [9, 16, 17, 24, 31, 32, 33, 48, 64, 65, 128, 200, 256])
@@ -1025,3 +1071,64 @@ def test_pinned_pool_bounded():
     gc.collect()
     pool.clear()
     assert pool.pinned_bytes == 0
+
+
+# ---- round 4: the single-process multi-device drop-in; C5 at full depth and size ------------
+
+@pytest.mark.parametrize("multi", ["0", "1"])
+def test_group_world1_matches_single_device(tmpdir_mod, monkeypatch, multi):
+    """Llama(path, args, devices=[0]) (l3_group_*: ncclCommInitAll, one thread) against the
+    single-device Llama on the same calls: prefill logits bit-identical, batched greedy steps and
+    generate_all ids equal, the lazy generate of one prompt equal (member 0's graph path), and
+    the group's member info.  multi=1 forces the multi-member path at N = 1 (per-member launch,
+    grouped RCCL gather, row interleave, ids-only gather for greedy steps), which the 1-GPU box
+    can otherwise never run."""
+    monkeypatch.setenv("L3_GROUP_MULTI_PATH", multi)
+    args = synth.stories15m(6)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "sharp")
+    ids = np.random.default_rng(61).integers(0, args.vocab_size, (6, 40))
+    single = llama3.Llama(path, args)
+    grp = llama3.Llama(path, args, devices=[0])
+    assert grp.group is not None and grp.group.n == 1
+    np.testing.assert_array_equal(grp(ids, 0), single(ids, 0))
+    np.testing.assert_array_equal(grp(ids[:5, :7], 40), single(ids[:5, :7], 40))
+    nxt_g, _ = grp.group.greedy_step(ids[:, :3], 47)
+    nxt_s, _ = single.context.greedy_step(ids[:, :3], 47)
+    np.testing.assert_array_equal(nxt_g, nxt_s)
+    info = grp.context.comm_info()
+    assert info["nranks"] == 1 and info["rank"] == 0 and len(info["busids"]) == 1
+    # greedy loops against the oracle (fresh models: the caches above hold other rows)
+    ref = orc.OracleModel(w, args)
+    want = orc.greedy_ids(ref, ids[:3, :5], 30)
+    g2 = llama3.Llama(path, args, devices=[0])
+    np.testing.assert_array_equal(g2.generate_all(ids[:3, :5], 30), want)
+    g3 = llama3.Llama(path, args, devices=[0])
+    lazy = np.concatenate(list(g3.generate(ids[:1, :5], 30)), axis=1)
+    np.testing.assert_array_equal(lazy, orc.greedy_ids(orc.OracleModel(w, args), ids[:1, :5], 30))
+    with pytest.raises(ValueError):
+        llama3.Llama(path, args, device=0, devices=[0])
+
+
+@pytest.mark.timeout(900)
+def test_c5_full_depth_full_size_rows_match_b1():
+    """BASELINE configs[4] exactly as the bench runs it — all 32 Llama-3-8B-shaped layers at
+    B = 64, L = 2048 (T = 131,072) — on the pool weights (synth.pool_weights, views of one 2 GB
+    uniform pool, handed to Llama as a mapping): every logit finite, and rows 0 and 63 equal to
+    the same rows run alone (B = 1) within 1e-5 (abs + rel; the B = 1 lm_head is the GEMV, another
+    reduction order over K = 4096).  The 32-layer oracle test above pins B = 1 against the
+    reference's arithmetic; this pins the full-size batch to B = 1 (llama3.py:163-211, 264-308)."""
+    args = synth.llama3_shape(n_layers=32, max_batch_size=64, max_seq_len=2048)
+    w = synth.pool_weights(args, synth.LLAMA3_HIDDEN, seed=0, pool_floats=1 << 29)
+    m = llama3.Llama(w, args)
+    del w
+    ids = np.random.default_rng(64).integers(0, args.vocab_size, (64, 2048))
+    out = m(ids, 0)
+    assert out.shape == (64, 1, args.vocab_size)
+    assert np.isfinite(out).all()
+    out = np.array(out)  # off the pinned pool before the next calls
+    errs = {}
+    for r in (0, 63):
+        one = m(ids[r:r + 1], 0)
+        errs[r] = float(np.max(np.abs(one.astype(np.float64) - out[r:r + 1])))
+        np.testing.assert_allclose(one, out[r:r + 1], rtol=1e-5, atol=1e-5)
+    print(f"c5 32 layers B=64 L=2048: rows vs B=1 max-abs {errs}, |logits| <= {float(np.abs(out).max()):.2f}")

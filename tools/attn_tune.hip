@@ -11,14 +11,7 @@
 #include <vector>
 
 #include "../llama3.np_amd/csrc/attn_kernel.h"
-#include "attn_ring.h"
-#include "attn_variants.h"
-#include "attn_v3.h"
-#include "attn_resident.h"
 #include "attn_research.h"
-#include "attn_pair.h"
-#include "attn_persist.h"
-#include "attn_rev.h"
 
 using namespace l3;
 
@@ -43,36 +36,6 @@ struct Variant {
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, dim3(256), 0, s, a); \
             }}
 
-// the product kernel on a multi-item grid: blocks resident at once = CAP (512 = 2 per CU)
-#define APERS(HD, QBW, G, KT, CAP)                                                            \
-    Variant{"persist<" #HD ",q" #QBW ",g" #G ",kt" #KT ",cap" #CAP ">", [](const AttnArgs& a, hipStream_t s) { \
-                launch_attn_persist<HD, QBW, G, KT>(a, s, CAP);                                    \
-            }}
-#define APERSQ(HD, QBW, G, KT, CAP)                                                           \
-    Variant{"persistq<" #HD ",q" #QBW ",g" #G ",kt" #KT ",cap" #CAP ">", [](const AttnArgs& a, hipStream_t s) { \
-                launch_attn_persist<HD, QBW, G, KT, true>(a, s, CAP);                              \
-            }}
-
-#define APAIR(HD, QBW, KT, MIR)                                                               \
-    Variant{"pair<" #HD ",q" #QBW ",kt" #KT ",mirror" #MIR ">", [](const AttnArgs& a, hipStream_t s) { \
-                constexpr int QW = 16 * QBW * 4;                                              \
-                dim3 grid((a.L + QW - 1) / QW, a.H / 2, a.B);                                 \
-                hipLaunchKernelGGL((attn_pair_kernel<HD, QBW, KT, MIR>), grid, dim3(512), 0, s, a); \
-            }}
-
-#define AREV(HD, KT)                                                                          \
-    Variant{"rev<" #HD ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) {                   \
-                dim3 grid((a.L + 255) / 256, a.H / 2, a.B);                                   \
-                hipLaunchKernelGGL((attn_rev_kernel<HD, KT>), grid, dim3(512), 0, s, a);        \
-            }}
-
-#define AVAR2(HD, QBW, G, KT, WPE)                                                            \
-    Variant{"v2<" #HD ",q" #QBW ",g" #G ",kt" #KT ",w" #WPE ">", [](const AttnArgs& a, hipStream_t s) { \
-                constexpr int QW = 16 * QBW * (4 / G);                                        \
-                dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
-                hipLaunchKernelGGL((attn_fwd_v2_kernel<HD, QBW, G, KT, WPE>), grid, dim3(256), 0, s, a); \
-            }}
-
 #define ADEF(HD, QBW, G, KT)                                                                  \
     Variant{"defer<" #HD ",q" #QBW ",g" #G ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) { \
                 constexpr int QW = 16 * QBW * (4 / G);                                        \
@@ -84,41 +47,6 @@ struct Variant {
     Variant{"v1<48,q4,kt64> abl" #ABL, [](const AttnArgs& a, hipStream_t s) {                  \
                 dim3 grid((a.L + 255) / 256, a.H, a.B);                                        \
                 hipLaunchKernelGGL((attn_research_kernel<48, 4, 1, 64, ABL>), grid, dim3(256), 0, s, a); \
-            }}
-
-#define AVAR3(QBW, KT, NS, WPE)                                                               \
-    Variant{"ring<q" #QBW ",kt" #KT ",ns" #NS ",w" #WPE ">", [](const AttnArgs& a, hipStream_t s) { \
-                constexpr int QW = 16 * QBW * 4;                                              \
-                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
-                hipLaunchKernelGGL((attn_ring_kernel<QBW, KT, NS, WPE>), grid, dim3(256), 0, s, a); \
-            }}
-
-#define AV3(NW, QBW, KT, LZ, SD)                                                              \
-    Variant{"v3<w" #NW ",q" #QBW ",kt" #KT ",lazy" #LZ ",skip" #SD ">", [](const AttnArgs& a, hipStream_t s) { \
-                constexpr int QW = 16 * QBW * NW;                                             \
-                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
-                hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD>), grid, dim3(64 * NW), 0, s, a); \
-            }}
-
-#define AV3I(NW, QBW, KT, LZ, SD)                                                             \
-    Variant{"v3ilv<w" #NW ",q" #QBW ",kt" #KT ",lazy" #LZ ",skip" #SD ">", [](const AttnArgs& a, hipStream_t s) { \
-                constexpr int QW = 16 * QBW * NW;                                             \
-                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
-                hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD, true>), grid, dim3(64 * NW), 0, s, a); \
-            }}
-
-#define AV3P(NW, QBW, KT, LZ, SD)                                                             \
-    Variant{"v3pipe<w" #NW ",q" #QBW ",kt" #KT ",lazy" #LZ ",skip" #SD ">", [](const AttnArgs& a, hipStream_t s) { \
-                constexpr int QW = 16 * QBW * NW;                                             \
-                dim3 grid((a.L + QW - 1) / QW, a.H, a.B);                                     \
-                hipLaunchKernelGGL((attn_v3_kernel<48, NW, QBW, KT, LZ, SD, true, true>), grid, dim3(64 * NW), 0, s, a); \
-            }}
-
-#define AVRES(HD, KMAX, TO)                                                                   \
-    Variant{"resident<" #HD ",kmax" #KMAX ",tileouter" #TO ">", [](const AttnArgs& a, hipStream_t s) { \
-                const int items = a.B * a.H;                                                  \
-                dim3 grid(items < 256 ? items : 256);                                         \
-                hipLaunchKernelGGL((attn_resident_kernel<HD, KMAX, TO>), grid, dim3(512), 0, s, a); \
             }}
 
 static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
@@ -226,35 +154,6 @@ int main(int argc, char** argv) {
         run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
         return 0;
     }
-    if (argc > 3 && std::string(argv[3]) == "rev") {  // second item's tiles in reverse order
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AREV(48, 64), APAIR(48, 4, 64, true),
-                                  AVAR(48, 4, 1, 64), AREV(48, 64)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M C3 half batch (one part of the split)", 128, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "pair") {  // two items per 8-wave workgroup
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), APAIR(48, 4, 64, true), APAIR(48, 4, 64, false),
-                                  AVAR(48, 4, 1, 64), APAIR(48, 4, 64, true)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "persist") {  // multi-item grids vs one block per item
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), APERS(48, 4, 1, 64, 512), APERSQ(48, 4, 1, 64, 512),
-                                  APERS(48, 4, 1, 64, 256), APERS(48, 4, 1, 64, 768), AVAR(48, 4, 1, 64),
-                                  APERS(48, 4, 1, 64, 512), APERSQ(48, 4, 1, 64, 512)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M C3 half batch (one part of the split)", 128, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M C4 on one GPU", 2048, 256, 6, 6, 48, v, 1, 3);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        std::vector<Variant> v5 = {AVAR(128, 1, 4, 32), APERS(128, 1, 4, 32, 512)};
-        run("Llama-3 shape B=4 L=2048", 4, 2048, 32, 8, 128, v5, 1, 2);
-        return 0;
-    }
     if (argc > 3 && std::string(argv[3]) == "stamps") {
         stamps(argc > 4 ? argv[4] : "gpurun_out/attn_stamps.bin", rounds);
         return 0;
@@ -278,19 +177,6 @@ int main(int argc, char** argv) {
         run("GQA n_rep 4, L=300 at 3", 2, 300, 8, 2, 48, {AVAR(48, 4, 4, 64), ADEF(48, 4, 4, 64)}, 1, 1, 3);
         return 0;
     }
-    if (argc > 3 && std::string(argv[3]) == "ring") {  // LDS-DMA ring variants against v1
-        run("stories15M C3", 256, 256, 6, 6, 48,
-            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 2, 2), AVAR3(4, 64, 3, 2), AVAR3(4, 64, 2, 3),
-             AVAR3(4, 32, 2, 3), AVAR3(4, 32, 3, 3), AVAR3(4, 32, 3, 2)},
-            rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48,
-            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 2, 2), AVAR3(4, 64, 3, 2), AVAR3(4, 32, 3, 3)}, 1, 1, 37);
-        run("stories15M L=100", 16, 100, 6, 6, 48,
-            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 2, 2), AVAR3(4, 64, 3, 2), AVAR3(4, 32, 3, 3)}, 1, 1);
-        run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48,
-            {AVAR(48, 4, 1, 64), AVAR3(4, 64, 3, 2)}, 1, 1, 19);
-        return 0;
-    }
     if (argc > 3 && std::string(argv[3]) == "abl") {  // ablations of v1 (timing only)
         run("stories15M C3 ablations", 256, 256, 6, 6, 48,
             {AVAR(48, 4, 1, 64), AABL(32), AABL(1), AABL(2), AABL(4), AABL(8), AABL(16), AABL(18), AABL(12),
@@ -302,48 +188,6 @@ int main(int argc, char** argv) {
         std::vector<Variant> v = {AVAR(48, 4, 1, 64), AABL(64), AABL(128), AABL(256), AVAR(48, 4, 1, 64)};
         run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
         run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "pipe") {  // LDS reads one group ahead
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AV3I(4, 4, 64, false, true), AV3P(4, 4, 64, false, true),
-                                  AV3P(4, 4, 64, true, true)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "res") {  // K/V resident, persistent, barrier-free
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AVRES(48, 256, false), AVRES(48, 256, true)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48, v, 1, 1, 19);
-        run("stories15M L=100", 16, 100, 6, 6, 48, v, 1, 1);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "ilv") {  // interleaved score chains
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AV3I(4, 4, 64, false, false), AV3I(4, 4, 64, false, true),
-                                  AV3I(4, 4, 64, true, true), AV3I(8, 2, 64, false, true), AV3I(8, 2, 32, false, true)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "v3") {  // lazy rescale / dead-group skip / 8 waves
-        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AV3(4, 4, 64, false, false), AV3(4, 4, 64, true, false),
-                                  AV3(4, 4, 64, false, true), AV3(4, 4, 64, true, true),
-                                  AV3(8, 2, 64, false, false), AV3(8, 2, 64, true, true), AV3(8, 2, 32, true, true)};
-        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
-        run("GQA n_rep 2, L=77 at 19", 8, 77, 6, 3, 48, v, 1, 1, 19);
-        return 0;
-    }
-    if (argc > 3 && std::string(argv[3]) == "v2") {  // v2 (per-key-group chains) against v1
-        run("stories15M C3", 256, 256, 6, 6, 48,
-            {AVAR(48, 4, 1, 64), AVAR2(48, 4, 1, 64, 2), AVAR2(48, 4, 1, 32, 2), AVAR2(48, 4, 1, 64, 1)},
-            rounds, iters);
-        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48,
-            {AVAR(48, 4, 1, 64), AVAR2(48, 4, 1, 64, 2)}, 1, 1, 37);
-        run("stories15M L=100", 16, 100, 6, 6, 48, {AVAR(48, 4, 1, 64), AVAR2(48, 4, 1, 64, 2)}, 1, 1);
-        run("Llama-3 shape (C5 slice)", 4, 2048, 32, 8, 128,
-            {AVAR(128, 1, 4, 32), AVAR2(128, 1, 4, 32, 2)}, rounds, 3);
         return 0;
     }
     run("stories15M C3", 256, 256, 6, 6, 48,

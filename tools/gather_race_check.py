@@ -2,7 +2,7 @@
 tests/test_gpu_parity.py::test_gather_pipelined_forwards_world1 and report every
 mismatch (which buffer, which rows / columns, and whose logits the wrong values are).
 Also runs the same forwards with no gather at all (control).  Usage:
-    python tools/gather_race_check.py [reps] [B] [L]"""
+    python tools/gather_race_check.py [reps] [B] [L] [overlap 0|1]"""
 import os
 import sys
 import tempfile
@@ -18,6 +18,7 @@ import synth  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 L = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+overlap = bool(int(sys.argv[4])) if len(sys.argv) > 4 else True  # l3_comm_set_overlap
 args = synth.stories15m(B)
 w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=0)
 tmp = tempfile.mkdtemp()
@@ -31,6 +32,7 @@ want = [ref(x, 0)[:, 0, :] for x in ids]
 m = llama3.Llama(path, args)
 ctx = m.context
 ctx.comm_init(1, 0, l3hip.comm_unique_id())
+ctx.set_comm_overlap(overlap)
 ids_dev = [ctx.alloc(x.nbytes) for x in ids]
 for d, x in zip(ids_dev, ids):
     ctx.h2d(d, x)
@@ -58,4 +60,4 @@ for rep in range(reps):
                     print(f"rep {rep} {mode} parts {parts} {nm}: {ne.sum()} wrong, rows "
                           f"{sorted(set(r.tolist()))}, cols {c.min()}..{c.max()}, "
                           f"% matching step 0/1/2: {whose}", flush=True)
-print(f"done: {reps} reps, {bad} bad buffers", flush=True)
+print(f"done: {reps} reps (overlap {overlap}), {bad} bad buffers", flush=True)

@@ -39,21 +39,12 @@ for s in "$@"; do
            step pmcD 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcD -o run --output-format csv -- tools/gemm_tune 1 2 ;;
     stamps) step stamps 300 tools/gemm_tune 1 1 stamps ;;
     attntune) step attntune 600 tools/attn_tune ;;
-    attnv2) step attnv2 300 tools/attn_tune 5 10 v2 ;;
     attnabl) step attnabl 300 tools/attn_tune 5 10 abl ;;
     attnpf2) step attnpf2 300 tools/attn_tune 5 10 pf2 ;;
     attnprio) step attnprio 300 tools/attn_tune 5 10 prio ;;
-    attnpipe) step attnpipe 300 tools/attn_tune 5 10 pipe ;;
-    attnres) step attnres 300 tools/attn_tune 5 10 res ;;
-    attnilv) step attnilv 300 tools/attn_tune 5 10 ilv ;;
-    attnv3) step attnv3 300 tools/attn_tune 5 10 v3 ;;
     attndefer) step attndefer 300 tools/attn_tune 5 10 defer ;;
-    attnring) step attnring 300 tools/attn_tune 5 10 ring ;;
     attnstamps) step attnstamps 120 tools/attn_tune 3 1 stamps gpurun_out/attn_stamps.bin ;;
     attnearly) step attnearly 300 tools/attn_tune 5 10 early ;;
-    attnrev) step attnrev 300 tools/attn_tune 5 10 rev ;;
-    attnpair) step attnpair 300 tools/attn_tune 5 10 pair ;;
-    attnpersist) step attnpersist 300 tools/attn_tune 5 10 persist ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
     floor) step floor 120 tools/launch_floor ;;
     hostprobe) step hostprobe 300 python tools/host_path_probe.py ;;
@@ -100,9 +91,6 @@ for s in "$@"; do
     c5deep) step c5deep 900 python -u -m pytest tests/test_gpu_parity.py -k c5_full_depth -x -v -s --timeout 900 --timeout-method thread ;;
     testsv) step tests 1200 python -u -m pytest tests -m gpu -v -rfP --timeout 900 --timeout-method thread ;;
     ragged) step ragged 300 python -u -m pytest tests/test_gpu_parity.py -k "ragged or cache_edges or head_dims or chunk" -x -q --timeout 300 --timeout-method thread ;;
-    gath3) L3_COMM_MODE=3 step gath3 300 python -u -m pytest tests/test_gpu_parity.py -k gather -x -q --timeout 300 --timeout-method thread ;;
-    race3) L3_COMM_MODE=3 step race3 300 python tools/gather_race_check.py 10 ;;
-    benchr3) L3_COMM_MODE=3 step benchr3 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
     benchr) step benchr 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
     benchrp0) L3_COMM_PRIORITY=0 step benchrp0 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl ;;
     benchrng) step benchrng 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --rccl --no-step-gather ;;
@@ -116,6 +104,11 @@ for s in "$@"; do
              step pmcgemmB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcgemmB -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 ;;
     attnprof) step attnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attnprof -o run --output-format csv -- tools/attn_tune 3 10 ;;
     loadprobe) step loadprobe 600 python tools/load_probe.py ;;
+    new4) step new4 1100 python -u -m pytest tests/test_gpu_parity.py -x -v -rfP -k "group or comm_info or gather or c4_full or c5_full_depth_full_size" --timeout 900 --timeout-method thread ;;
+    single1) step single1 300 python bench.py --single-process --gpus 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    single1m) L3_GROUP_MULTI_PATH=1 step single1m 300 python bench.py --single-process --gpus 1 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    spawn1o) step spawn1o 300 python bench.py --spawn --rccl --comm-overlap --steps 20 --warmup 3 --no-cpu-baseline ;;
+    gathov) step gathov 300 python tools/gather_race_check.py 10 ;;
     cabi) step cabi 300 python -u -m pytest tests/test_c_abi_gpu.py -x -v --timeout 120 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
