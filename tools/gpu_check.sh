@@ -47,6 +47,7 @@ for s in "$@"; do
     attnearly) step attnearly 300 tools/attn_tune 5 10 early ;;
     profr) step profr 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profr -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --rccl ;;
     floor) step floor 120 tools/launch_floor ;;
+    handoff) step handoff 180 tools/handoff_chain ;;
     hostprobe) step hostprobe 300 python tools/host_path_probe.py ;;
     decode) step decode 300 python tools/bench_decode.py ;;
     decode32) L3_GEMV_LPU=32 step decode32 300 python tools/bench_decode.py ;;
