@@ -1,0 +1,521 @@
+// Persistent batch-1 greedy decode step (llama3.py:316-320 at B = 1, L = 1): the whole step —
+// every layer's RMSNorm + QKV + RoPE + KV append, attention, O-proj + residual, RMSNorm + gate|up
+// + SwiGLU, down + residual, then the final norm + lm_head and the greedy argmax — as ONE launch
+// instead of 25 graph-replayed kernels.
+//
+// Why: a batch-1 stories15M step is ~60 MB of L2/MALL-resident weights and a chain of ~30
+// all-to-all dependencies (every output of a stage needs the stage's whole input vector).  As
+// separate launches each dependency costs a kernel boundary plus the kernel's dependent memory
+// round trips (tools/launch_floor: 1.8 us empty, 2.4 us with one load round trip; the product
+// step averages 3.8 us per kernel).  Inside one launch an all-to-all hand-off measured 1.85-2.3
+// us (tools/handoff_chain, profiles/r04_handoff_chain.log), about a boundary — so the gain must
+// come from what a boundary forbids: every workgroup issues the NEXT stage's weight loads right
+// after publishing the current stage, and they land while it waits for the hand-off.
+//
+// Hand-offs (cdna_hip_programming.md Guideline 16, R2): every stage output value travels as one
+// 8-byte {tag, value} granule written by ONE agent-scope relaxed atomic store (sc1 write-through);
+// consumers re-read the granules they need with agent-scope relaxed loads (sc1, L1-bypassing)
+// until every tag equals the launch's epoch.  Each (layer, stage) has its own granule slab, so no
+// slab is rewritten inside a launch; the epoch (a device word, +1 at the end of every launch by
+// workgroup 0, after every other workgroup has published its last value) makes the previous
+// launch's granules stale without a memset.  Only values produced in THIS launch travel as
+// granules; everything older (weights, the KV rows of earlier positions, the token id) is read
+// with plain loads, which a kernel boundary makes visible.  Spins are bounded: a workgroup that
+// waits ~1 s sets the error word (host-mapped) and leaves, so a fault ends the launch instead of
+// hanging it; the host checks the word after every synchronised step.
+//
+// Work split (grid = 256 workgroups x 256 threads, all resident: 1 per CU by resources): the layer
+// stages run on workgroups 0..GL-1 (GL = 64, eight per XCD under round-robin dispatch); the
+// attention of head h on workgroup h; the lm_head's 32000 rows on all 256 (workgroups >= GL load
+// their rows while the layers run).  GEMV stages: 16 lanes per output unit (a row, or a RoPE /
+// gate-up row pair), the unit's W rows in registers, the input vector staged once per workgroup
+// in LDS.
+#include "kernels.h"
+
+namespace l3 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64;
+
+namespace persist {
+
+constexpr int NT = 256;          // threads per workgroup
+constexpr int LPR = 16;          // lanes per unit in the GEMV stages
+constexpr int UPP = NT / LPR;    // units per pass
+
+__device__ __forceinline__ void gput(u64* g, unsigned tag, float v) {
+    __hip_atomic_store(g, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 gget(u64* g) {
+    return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct Ctx {
+    const DecodePersistArgs& p;
+    unsigned tag;
+    int pos;
+    volatile int* bad;  // LDS flag: this workgroup gave up on a hand-off
+    float* red;         // LDS scratch [NT]
+};
+
+__device__ __forceinline__ void give_up(const Ctx& c) {
+    *c.bad = 1;
+    __hip_atomic_store(c.p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(c.p.epoch + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
+}
+
+// granules g[idx(i)] for i < n into dst[i] (LDS), every thread its i = tid + NT*k, all of a
+// thread's loads in flight per pass; re-read until every tag is the launch's.  Ends with a
+// workgroup barrier; false if this workgroup gave up (caller returns).
+template <int PER, typename Idx>
+__device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
+    const int tid = threadIdx.x;
+    bool ok = false;
+    for (unsigned spin = 0;; ++spin) {
+        ok = true;
+        u64 x[PER];
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = tid + NT * k;
+            x[k] = i < n ? gget(g + idx(i)) : ((u64)c.tag << 32);
+        }
+#pragma unroll
+        for (int k = 0; k < PER; ++k) ok &= (unsigned)(x[k] >> 32) == c.tag;
+        if (ok) {
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const int i = tid + NT * k;
+                if (i < n) dst[i] = __uint_as_float((unsigned)x[k]);
+            }
+            break;
+        }
+        if (spin > (1u << 20) || *c.bad) {
+            give_up(c);
+            break;
+        }
+        if (sleep == 1) __builtin_amdgcn_s_sleep(1);
+        else __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+    return !*c.bad;
+}
+
+template <typename Idx>
+__device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
+    if (n <= NT) return sweep<1>(c, g, n, dst, idx, sleep);
+    if (n <= 2 * NT) return sweep<2>(c, g, n, dst, idx, sleep);
+    return sweep<4>(c, g, n, dst, idx, sleep);  // n <= 1024 (eligibility)
+}
+
+// block sum of one value per thread (every thread gets it)
+__device__ __forceinline__ float block_sum(const Ctx& c, float v) {
+    v = group_sum<64>(v);
+    const int tid = threadIdx.x;
+    __syncthreads();
+    if ((tid & 63) == 0) c.red[tid >> 6] = v;
+    __syncthreads();
+    return (c.red[0] + c.red[1]) + (c.red[2] + c.red[3]);
+}
+__device__ __forceinline__ float block_max(const Ctx& c, float v) {
+    v = group_max<64>(v);
+    const int tid = threadIdx.x;
+    __syncthreads();
+    if ((tid & 63) == 0) c.red[tid >> 6] = v;
+    __syncthreads();
+    return fmaxf(fmaxf(c.red[0], c.red[1]), fmaxf(c.red[2], c.red[3]));
+}
+
+// 1 / rms of the LDS vector x[0..n) (RMSNorm, llama3.py:111-114; the weight is folded into W)
+__device__ __forceinline__ float inv_rms(const Ctx& c, const float* x, int n) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < n; i += NT) s += x[i] * x[i];
+    s = block_sum(c, s);
+    return __builtin_amdgcn_rsqf(s / (float)n + c.p.eps);
+}
+
+// W rows of one unit into registers: lane j of the unit holds float4s k4 = j + LPR * t, t < NC
+template <int ROWS, int NC>
+__device__ __forceinline__ void load_rows(const float* W, const int (&row)[ROWS], int K4, bool valid,
+                                          f32x4 (&w)[ROWS][NC]) {
+    const int j = threadIdx.x % LPR;
+    const f32x4* W4 = reinterpret_cast<const f32x4*>(W);
+#pragma unroll
+    for (int t = 0; t < NC; ++t) {
+        const int k4 = j + LPR * t;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r)
+            w[r][t] = (valid && k4 < K4) ? W4[(int64_t)row[r] * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+template <int ROWS, int NC>
+__device__ __forceinline__ void dot_rows(const f32x4 (&w)[ROWS][NC], const float* x, int K4, float (&acc)[ROWS]) {
+    const int j = threadIdx.x % LPR;
+    const f32x4* X4 = reinterpret_cast<const f32x4*>(x);
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NC; ++t) {
+        const int k4 = j + LPR * t;
+        if (k4 >= K4) break;
+        const f32x4 xv = X4[k4];
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) acc[r] += w[r][t].x * xv.x + w[r][t].y * xv.y + w[r][t].z * xv.z + w[r][t].w * xv.w;
+    }
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r] = group_sum<LPR>(acc[r]);
+}
+
+// this workgroup's unit range of a layer stage with n units over GL workgroups (one pass: the
+// eligibility keeps ceil(n / GL) <= UPP)
+__device__ __forceinline__ int stage_unit(const DecodePersistArgs& p, int n, int wg, bool& valid) {
+    const int per = (n + p.GL - 1) / p.GL;
+    const int i = threadIdx.x / LPR;
+    const int u = wg * per + i;
+    valid = i < per && u < n;
+    return valid ? u : 0;
+}
+
+}  // namespace persist
+
+// One launch = one decode step.  Granule slab per layer: [qkv | o | h1 | hid | h2], then the
+// lm_head partials [2 * gridDim.x].
+// NCD / NCF: float4 per lane of a W row with K = D / K = FD (>= ceil(K / 64)); KPF >= HD / 4; LMPF:
+// lm_head passes of 16 rows each workgroup holds in registers
+template <int NCD, int NCF, int KPF, int LMPF>
+__global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArgs p) {
+    using namespace persist;
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    __shared__ int bad_s;
+    __shared__ float red_s[NT];
+    const int D = p.D, HD = p.HD, H = p.H, KVH = p.KVH, FD = p.FD;
+    const int qdim = H * HD, kvdim = KVH * HD, qkvn = qdim + 2 * kvdim;
+    float* hin = sm;              // [D]  layer input (residual of the O-proj)
+    float* h1s = hin + p.Dp;      // [D]  FFN input (residual of the down-proj)
+    float* xs = h1s + p.Dp;       // [max(qkvn, FD, qdim)] stage input
+    float* sc = xs + p.Xp;        // [Smax] attention scores
+    const int tid = threadIdx.x, wg = blockIdx.x, G = gridDim.x;
+    if (tid == 0) bad_s = 0;
+    const unsigned tag = p.epoch[0];
+    const int pos = p.st->pos;
+    const int id = p.ids[0];
+    // an earlier launch gave up (epoch[1], sticky): do nothing, the host reports it
+    if (p.epoch[1]) return;
+    __syncthreads();
+    Ctx c{p, tag, pos, &bad_s, red_s};
+    const int64_t slab = (int64_t)qkvn + qdim + D + FD + D;
+    u64* lm_g = p.gran + slab * p.n_layers;
+    const int K4d = D / 4, K4f = FD / 4, K4q = qdim / 4;
+    const bool layer_wg = wg < p.GL;
+
+    // lm_head rows of this workgroup: [r0, r1); unit = one row, LPR lanes
+    const int lm_per = (p.VS + G - 1) / G, lm_r0 = wg * lm_per, lm_r1 = min(p.VS, lm_r0 + lm_per);
+    const int lm_passes = (lm_r1 - lm_r0 + UPP - 1) / UPP;
+    f32x4 lw[LMPF][1][NCD];
+    auto lm_load = [&]() {
+#pragma unroll
+        for (int ps = 0; ps < LMPF; ++ps) {
+            const int r = lm_r0 + ps * UPP + tid / LPR;
+            const int row[1] = {min(r, p.VS - 1)};
+            load_rows<1, NCD>(p.lm_head, row, K4d, ps < lm_passes && r < lm_r1, lw[ps]);
+        }
+    };
+    if (!layer_wg) lm_load();  // nothing else to do: the rows land while the layers run
+
+    for (int li = 0; li < p.n_layers && layer_wg; ++li) {
+        u64* g_qkv = p.gran + slab * li;
+        u64* g_o = g_qkv + qkvn;
+        u64* g_h1 = g_o + qdim;
+        u64* g_hid = g_h1 + D;
+        u64* g_h2 = g_hid + FD;
+        const float* wqkv = p.wqkv[li];
+        float* ck = p.cache_k[li];
+        float* cv = p.cache_v[li];
+        // ---- stage A: RMSNorm + QKV + RoPE + KV append (llama3.py:248, 166-185) -------------
+        {
+            bool valid;
+            const int u = stage_unit(p, qkvn / 2, wg, valid);  // RoPE pair (rows 2u, 2u + 1)
+            const int row[2] = {2 * u, 2 * u + 1};
+            f32x4 w[2][NCD];
+            load_rows<2, NCD>(wqkv, row, K4d, valid, w);
+            const int col = 2 * u;
+            const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
+            const int cc = col - (sec == 0 ? 0 : sec == 1 ? qdim : qdim + kvdim);
+            const int head = cc / HD, d = cc - head * HD;
+            float2 cs = {1.f, 0.f};
+            if (sec < 2) {
+                const int t = pos * (HD >> 1) + (d >> 1);
+                cs = float2{p.rope_cos[t], p.rope_sin[t]};
+            }
+            float* cache = sec == 1 ? ck : cv;
+            const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
+            float2 old = {0.f, 0.f};
+            if (p.kv_bak && sec > 0 && valid) old = *reinterpret_cast<const float2*>(cache + coff);
+            // the layer input: the token's embedding row (llama3.py:287), else the previous
+            // layer's output granules
+            if (li == 0) {
+                for (int i = tid; i < D; i += NT) hin[i] = p.emb[(int64_t)id * D + i];
+                __syncthreads();
+            } else if (!sweep_n(c, p.gran + slab * (li - 1) + qkvn + qdim + D + FD, D, hin, [](int i) { return i; })) {
+                goto done;
+            }
+            const float rs = inv_rms(c, hin, D);
+            float acc[2];
+            dot_rows<2, NCD>(w, hin, K4d, acc);
+            if (valid && tid % LPR == 0) {
+                const float v0 = acc[0] * rs, v1 = acc[1] * rs;
+                const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
+                const float s = sec == 0 ? p.q_scale : 1.0f;
+                gput(g_qkv + col, tag, r0 * s);
+                gput(g_qkv + col + 1, tag, r1 * s);
+                if (sec > 0) {
+                    if (p.kv_bak)  // [pos % KV_BAK_SLOTS][k, v][1][KVH][HD]: the slot it overwrites
+                        *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer +
+                                                   (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d) = old;
+                    *reinterpret_cast<float2*>(cache + coff) = float2{r0, r1};
+                }
+            }
+        }
+        // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
+        if (wg < H) {
+            const int h = wg, kvh = h / (H / KVH);
+            const int D4 = HD / 4, R = NT / D4;          // PV: R key groups x D4 float4 columns
+            const int rg = tid / D4, d4 = tid - rg * D4;
+            const f32x4* K4p = reinterpret_cast<const f32x4*>(ck + (int64_t)kvh * p.Smax * HD);
+            const f32x4* V4p = reinterpret_cast<const f32x4*>(cv + (int64_t)kvh * p.Smax * HD);
+            // keys before pos come from the cache (earlier launches); key pos from the granules
+            constexpr int VPF = 8;
+            f32x4 kr[KPF];
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) kr[i] = (i < D4 && tid < pos) ? K4p[(int64_t)tid * D4 + i] : f32x4{0.f, 0.f, 0.f, 0.f};
+            f32x4 vr[VPF];
+#pragma unroll
+            for (int t = 0; t < VPF; ++t) {
+                const int k = rg + t * R;
+                vr[t] = (rg < R && k < pos) ? V4p[(int64_t)k * D4 + d4] : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            float* qs = xs;                              // q | k_new | v_new of this head
+            const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
+            if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
+                goto done;
+            const f32x4* q4 = reinterpret_cast<const f32x4*>(qs);
+            const f32x4* kn4 = reinterpret_cast<const f32x4*>(qs + HD);
+            const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
+            const int S = pos + 1;
+            // key tid from the prefetched row (rows past HD are zero: the q4 reads past HD land
+            // in the k / v part of qs and add nothing)
+            float s_own = 0.f;
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) {
+                const f32x4 b = q4[i];
+                s_own += kr[i].x * b.x + kr[i].y * b.y + kr[i].z * b.z + kr[i].w * b.w;
+            }
+            float m = -INFINITY;
+            for (int k = tid; k < S; k += NT) {
+                float s = 0.f;
+                if (k == pos) {
+                    for (int i = 0; i < D4; ++i) {
+                        const f32x4 a = kn4[i], b = q4[i];
+                        s += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+                    }
+                } else if (k < NT) {
+                    s = s_own;
+                } else {
+                    for (int i = 0; i < D4; ++i) {
+                        const f32x4 a = K4p[(int64_t)k * D4 + i], b = q4[i];
+                        s += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+                    }
+                }
+                sc[k] = s;
+                m = fmaxf(m, s);
+            }
+            m = block_max(c, m);
+            float l = 0.f;
+            for (int k = tid; k < S; k += NT) {
+                const float e = __builtin_amdgcn_exp2f(sc[k] - m);  // q carries log2(e) / sqrt(HD)
+                sc[k] = e;
+                l += e;
+            }
+            l = block_sum(c, l);  // its barriers also publish sc
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            if (rg < R) {
+#pragma unroll
+                for (int t = 0; t < VPF; ++t) {
+                    const int k = rg + t * R;
+                    if (k < pos) acc += sc[k] * vr[t];
+                }
+                for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
+                if (pos % R == rg) acc += sc[pos] * vn4[d4];
+            }
+            __syncthreads();  // xs (q) may be reused as the reduction buffer below
+            f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
+            if (rg < R) part[rg * D4 + d4] = acc;
+            __syncthreads();
+            if (tid < D4) {
+                f32x4 o = {0.f, 0.f, 0.f, 0.f};
+                for (int r = 0; r < R; ++r) o += part[r * D4 + tid];
+                o *= 1.0f / l;
+                gput(g_o + qo + 4 * tid + 0, tag, o.x);
+                gput(g_o + qo + 4 * tid + 1, tag, o.y);
+                gput(g_o + qo + 4 * tid + 2, tag, o.z);
+                gput(g_o + qo + 4 * tid + 3, tag, o.w);
+            }
+        }
+        // ---- stage C: O-proj + residual (llama3.py:211, 253) --------------------------------
+        {
+            bool valid;
+            const int u = stage_unit(p, D, wg, valid);
+            const int row[1] = {u};
+            f32x4 w[1][NCD];
+            load_rows<1, NCD>(p.wo[li], row, K4q, valid, w);
+            if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
+            float acc[1];
+            dot_rows<1, NCD>(w, xs, K4q, acc);
+            if (valid && tid % LPR == 0) gput(g_h1 + u, tag, hin[u] + acc[0]);
+        }
+        // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) -----------------------
+        {
+            bool valid;
+            const int u = stage_unit(p, FD, wg, valid);  // hidden unit: fused rows 32(u/16) + u%16, +16
+            const int row[2] = {32 * (u / 16) + u % 16, 32 * (u / 16) + u % 16 + 16};
+            f32x4 w[2][NCD];
+            load_rows<2, NCD>(p.wgu[li], row, K4d, valid, w);
+            if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
+            const float rs = inv_rms(c, h1s, D);
+            float acc[2];
+            dot_rows<2, NCD>(w, h1s, K4d, acc);
+            if (valid && tid % LPR == 0) {
+                const float g = acc[0] * rs, up = acc[1] * rs;
+                gput(g_hid + u, tag, g * __builtin_amdgcn_rcpf(1.0f + __expf(-g)) * up);
+            }
+        }
+        // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
+        {
+            bool valid;
+            const int u = stage_unit(p, D, wg, valid);
+            const int row[1] = {u};
+            f32x4 w[1][NCF];
+            load_rows<1, NCF>(p.wd[li], row, K4f, valid, w);
+            if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
+            float acc[1];
+            dot_rows<1, NCF>(w, xs, K4f, acc);
+            if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);
+        }
+    }
+    if (layer_wg) lm_load();  // in flight while the last layer's output arrives
+
+    // ---- final RMSNorm + lm_head (llama3.py:304-307) + this workgroup's argmax (:320) ---------
+    {
+        u64* g_last = p.gran + slab * (p.n_layers - 1) + qkvn + qdim + D + FD;
+        if (!layer_wg && tid == 0) {  // a long wait: one lane polls the last granule, sleeping
+            for (unsigned spin = 0; (unsigned)(gget(g_last + D - 1) >> 32) != tag; ++spin) {
+                if (spin > (1u << 20)) break;
+                __builtin_amdgcn_s_sleep(16);
+            }
+        }
+        if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, layer_wg ? 1 : 8)) goto done;
+        const float rs = inv_rms(c, xs, D);
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int ps = 0; ps < lm_passes; ++ps) {
+            const int r = lm_r0 + ps * UPP + tid / LPR;
+            float acc[1];
+            if (ps < LMPF) {
+                // a compile-time index into lw: unrolled select
+#pragma unroll
+                for (int q = 0; q < LMPF; ++q)
+                    if (q == ps) dot_rows<1, NCD>(lw[q], xs, K4d, acc);
+            } else {
+                f32x4 w[1][NCD];
+                const int row[1] = {min(r, p.VS - 1)};
+                load_rows<1, NCD>(p.lm_head, row, K4d, r < lm_r1, w);
+                dot_rows<1, NCD>(w, xs, K4d, acc);
+            }
+            const float v = acc[0] * rs;
+            if (r < lm_r1 && argmax_better(v, r, best, bi)) { best = v; bi = r; }
+        }
+        group_argmax<64>(best, bi, tid & 63);
+        __shared__ float bv_s[4];
+        __shared__ int bi_s[4];
+        if ((tid & 63) == 0) { bv_s[tid >> 6] = best; bi_s[tid >> 6] = bi; }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w2 = 1; w2 < 4; ++w2)
+                if (argmax_better(bv_s[w2], bi_s[w2], best, bi)) { best = bv_s[w2]; bi = bi_s[w2]; }
+            gput(lm_g + 2 * wg, tag, best);
+            gput(lm_g + 2 * wg + 1, tag, __int_as_float(bi));
+        }
+    }
+    // ---- workgroup 0: the step's greedy id from the G partials; generate history, position ----
+    if (wg == 0) {
+        float* pv = xs;  // [2G]
+        if (sweep_n(c, lm_g, 2 * G, pv, [](int i) { return i; })) {
+            float best = -INFINITY;
+            int bi = 0x7fffffff;
+            for (int i = tid; i < G; i += NT)
+                if (argmax_better(pv[2 * i], __float_as_int(pv[2 * i + 1]), best, bi)) {
+                    best = pv[2 * i];
+                    bi = __float_as_int(pv[2 * i + 1]);
+                }
+            group_argmax<64>(best, bi, tid & 63);
+            __shared__ float fb[4];
+            __shared__ int fi[4];
+            if ((tid & 63) == 0) { fb[tid >> 6] = best; fi[tid >> 6] = bi; }
+            __syncthreads();
+            if (tid == 0) {
+                for (int w2 = 1; w2 < 4; ++w2)
+                    if (argmax_better(fb[w2], fi[w2], best, bi)) { best = fb[w2]; bi = fi[w2]; }
+                p.ids[0] = bi;
+                DecState* st = p.st;
+                const int q = pos - st->hist_base;
+                if (st->hist && q >= 0 && q < st->hist_cap) st->hist[q] = bi;
+                st->pos = pos + 1;
+            }
+        }
+    }
+done:
+    if (wg == 0 && tid == 0) *p.epoch = tag + 1;  // every workgroup has read its last granule
+}
+
+// instantiated shapes: chunk counts rounded up (the loads past K are predicated off)
+static int ncd_of(int D) { const int n = (D + 63) / 64; return n <= 1 ? 1 : n <= 5 ? 5 : n <= 8 ? 8 : 0; }
+static int ncf_of(int FD) { const int n = (FD + 63) / 64; return n <= 3 ? 3 : n <= 12 ? 12 : n <= 16 ? 16 : 0; }
+
+bool decode_persist_ok(const DecodePersistArgs& a) {
+    const int qkvn = (a.H + 2 * a.KVH) * a.HD;
+    return a.D % 4 == 0 && a.FD % 4 == 0 && a.HD % 4 == 0 && a.HD >= 4 && a.HD <= 64 && a.H <= a.GL &&
+           a.H % a.KVH == 0 && a.H * a.HD == a.D && ncd_of(a.D) && ncf_of(a.FD) && qkvn % 2 == 0 &&
+           (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD + a.GL - 1) / a.GL <= persist::UPP &&
+           (a.D + a.GL - 1) / a.GL <= persist::UPP && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
+           a.n_layers >= 1 && a.GL >= 1 && a.GL <= 256;
+}
+
+// Grid of one decode step: one workgroup per CU (256 on MI355X; every one resident: 1 per CU by
+// its registers), dynamic LDS sized by the shape
+hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s) {
+    if (!decode_persist_ok(a)) return hipErrorNotSupported;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return hipErrorNotSupported;
+    const int grid = cus < 256 ? cus : 256;
+    if (grid < a.GL) return hipErrorNotSupported;
+    const size_t lds = ((size_t)2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
+    const int ncd = ncd_of(a.D), ncf = ncf_of(a.FD);
+#define L3_PERSIST(NCD, NCF, KPF, LMPF)                                                            \
+    if (ncd == NCD && ncf == NCF) {                                                                \
+        hipLaunchKernelGGL((decode_persist_kernel<NCD, NCF, KPF, LMPF>), dim3(grid), dim3(256), lds, s, a); \
+        return hipGetLastError();                                                                  \
+    }
+    L3_PERSIST(1, 3, 16, 8)   // tiny models (tests)
+    L3_PERSIST(5, 12, 12, 8)  // stories15M: D 288, FD 768, HD 48
+    L3_PERSIST(5, 16, 16, 4)
+    L3_PERSIST(8, 16, 16, 2)
+    L3_PERSIST(1, 12, 16, 8)
+    L3_PERSIST(5, 3, 16, 8)
+    L3_PERSIST(8, 12, 16, 2)
+#undef L3_PERSIST
+    return hipErrorNotSupported;
+}
+
+}  // namespace l3

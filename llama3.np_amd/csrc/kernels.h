@@ -10,7 +10,8 @@ namespace l3 {
 // (DESIGN.md decisions table) and the knobs exist only to re-run those A/B measurements.
 //   runtime.hip  L3_BATCH_SPLIT (2), L3_LAST_LAYER_ALL_ROWS (0), L3_DECODE_FUSE_O (1),
 //                L3_LM_AMAX (1), L3_DECODE_FOLD_ARGMAX (1), L3_DECODE_SPECULATE (1), L3_DECODE_GRAPH_STEPS (8),
-//                L3_DECODE_GRAPH (1), L3_COMM_MODE (1), L3_COMM_PRIORITY (1), L3_GROUP_MULTI_PATH (0)
+//                L3_DECODE_GRAPH (1), L3_COMM_MODE (1), L3_COMM_PRIORITY (1), L3_GROUP_MULTI_PATH (0),
+//                L3_DECODE_PERSIST (0)
 //   gemm.hip     L3_SPLITK (1), L3_SPLITK_CFG (0), L3_SPLITK_BLOCKS (1024), L3_SPLITK_MINKT (8),
 //                L3_GEMV_NT (1), L3_GEMV_LPU (0 = by shape), L3_GEMV_MR (by shape), L3_SKINNY (1),
 //                L3_SKINNY_MIN (9)
@@ -235,6 +236,33 @@ template <typename Args>
 __device__ __forceinline__ int start_of(const Args& p) {
     return p.pos_dev ? *p.pos_dev : p.start_pos;
 }
+
+// Persistent batch-1 decode step (decode_persist.hip): one launch runs a whole greedy step —
+// every layer, the lm_head and the argmax — with in-launch hand-offs between the stages
+struct DecodePersistArgs {
+    int D, H, KVH, HD, FD, VS, n_layers, Smax;
+    int GL;                        // workgroups that run the layer stages (the lm_head uses all 256)
+    int Dp, Xp;                    // LDS floats: per D-vector, per stage-input vector (multiples of 4)
+    float eps, q_scale;
+    const float* emb;              // [VS, D]
+    const float* lm_head;          // [VS, D], final norm folded
+    const float* const* wqkv;      // per layer (device arrays of device pointers); norms folded
+    const float* const* wo;
+    const float* const* wgu;
+    const float* const* wd;
+    float* const* cache_k;         // per layer [maxB, KVH, Smax, HD]; batch row 0
+    float* const* cache_v;
+    const float* rope_cos; const float* rope_sin;
+    float* kv_bak;                 // null, or the run-ahead undo slots (GemmArgs::kv_bak layout, B = 1)
+    int64_t bak_layer;             // floats per layer of kv_bak
+    int32_t* ids;                  // [1]: this step's token id in, the next step's out
+    DecState* st;                  // pos (read; +1), generate history
+    unsigned long long* gran;      // granule slabs (decode_persist.hip), zeroed at allocation
+    unsigned* epoch;               // [0] granule tag of the next launch (starts at 1); [1] sticky failure
+    unsigned* err;                 // host-mapped: set to 1 when a workgroup gave up on a hand-off
+};
+bool decode_persist_ok(const DecodePersistArgs& a);
+hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s);
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);

@@ -203,6 +203,13 @@ struct l3_ctx {
     std::deque<SpecChunk> spec_q;
     std::vector<hipEvent_t> spec_free;  // event pool (timing events)
     int64_t spec_hits = 0;
+    // persistent batch-1 decode step (decode_persist.hip): a captured step is one launch of
+    // decode_persist_kernel instead of 25 kernels (L3_DECODE_PERSIST; persist_setup)
+    void* persist_mem = nullptr;     // per-layer pointer arrays, epoch word, granule slabs
+    unsigned* persist_err = nullptr; // host-mapped error word (device writes it on a timeout)
+    unsigned* persist_err_dev = nullptr;
+    DecodePersistArgs persist{};
+    bool persist_ready = false;
 };
 
 // ---------------------------------------------------------------------------------------
@@ -430,6 +437,8 @@ extern "C" int l3_destroy(l3_ctx* c) {
     for (auto& q : c->spec_q) { (void)hipEventDestroy(q.ev0); (void)hipEventDestroy(q.ev1); (void)hipEventDestroy(q.ev); }
     for (hipEvent_t e : c->spec_free) (void)hipEventDestroy(e);
     dfree(c->spec_hist);
+    dfree(c->persist_mem);
+    if (c->persist_err) (void)hipHostFree(c->persist_err);
     if (c->spec_ids) (void)hipHostFree(c->spec_ids);
     if (c->hist_host) (void)hipHostFree(c->hist_host);
     for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i) {
@@ -941,18 +950,96 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
     return 0;
 }
 
+// Persistent batch-1 decode step (decode_persist.hip): L3_DECODE_PERSIST=1 (A/B) and a shape the
+// kernel takes (decode_persist_ok).  Its buffers are made once, with the stream idle.
+static bool persist_wanted(l3_ctx* c, int B) {
+    static const bool on = env_knob("L3_DECODE_PERSIST", 0) != 0;
+    if (!on || B != 1 || c->layers.empty() || !c->dec_state) return false;
+    if (c->persist_ready) return true;
+    DecodePersistArgs a{};
+    a.D = c->d.dim; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads; a.HD = c->HD; a.FD = c->d.hidden_dim;
+    a.VS = c->d.vocab_size; a.n_layers = (int)c->layers.size(); a.Smax = c->d.max_seq_len; a.GL = 64;
+    return decode_persist_ok(a);
+}
+
+static int persist_setup(l3_ctx* c) {
+    if (c->persist_ready) return 0;
+    DecodePersistArgs& a = c->persist;
+    a = DecodePersistArgs{};
+    const int nl = (int)c->layers.size();
+    a.D = c->d.dim; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads; a.HD = c->HD; a.FD = c->d.hidden_dim;
+    a.VS = c->d.vocab_size; a.n_layers = nl; a.Smax = c->d.max_seq_len; a.GL = 64;
+    a.Dp = (a.D + 3) & ~3;
+    int xp = c->qkvn > a.FD ? c->qkvn : a.FD;
+    if (xp < 3 * a.HD) xp = 3 * a.HD;
+    if (xp < 512) xp = 512;  // the final argmax's 2 x 256 partials
+    a.Xp = (xp + 3) & ~3;
+    a.eps = c->d.norm_eps;
+    a.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
+    a.emb = c->emb; a.lm_head = c->lm_head; a.rope_cos = c->rope_cos; a.rope_sin = c->rope_sin;
+    a.bak_layer = (int64_t)KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD;
+    const int64_t slab = (int64_t)c->qkvn + c->qdim + a.D + a.FD + a.D;
+    const size_t ptr_bytes = (size_t)6 * nl * sizeof(void*);
+    const size_t gran_off = (ptr_bytes + 16 + 255) & ~(size_t)255;
+    const size_t gran_bytes = (size_t)(slab * nl + 2 * 256) * 8;
+    HIP_TRY(hipMalloc(&c->persist_mem, gran_off + gran_bytes));
+    HIP_TRY(hipMemset(c->persist_mem, 0, gran_off + gran_bytes));
+    std::vector<const void*> ptrs((size_t)6 * nl);
+    for (int i = 0; i < nl; ++i) {
+        const Layer& L = c->layers[(size_t)i];
+        ptrs[(size_t)i] = L.wqkv; ptrs[(size_t)nl + i] = L.wo; ptrs[(size_t)2 * nl + i] = L.wgu;
+        ptrs[(size_t)3 * nl + i] = L.wd; ptrs[(size_t)4 * nl + i] = L.cache_k; ptrs[(size_t)5 * nl + i] = L.cache_v;
+    }
+    HIP_TRY(hipMemcpy(c->persist_mem, ptrs.data(), ptr_bytes, hipMemcpyHostToDevice));
+    char* base = static_cast<char*>(c->persist_mem);
+    auto arr = [&](int k) { return reinterpret_cast<void* const*>(base) + (size_t)k * nl; };
+    a.wqkv = reinterpret_cast<const float* const*>(arr(0));
+    a.wo = reinterpret_cast<const float* const*>(arr(1));
+    a.wgu = reinterpret_cast<const float* const*>(arr(2));
+    a.wd = reinterpret_cast<const float* const*>(arr(3));
+    a.cache_k = reinterpret_cast<float* const*>(arr(4));
+    a.cache_v = reinterpret_cast<float* const*>(arr(5));
+    a.epoch = reinterpret_cast<unsigned*>(base + ptr_bytes);
+    const unsigned one = 1;  // tag 0 is what the zeroed slabs hold
+    HIP_TRY(hipMemcpy(a.epoch, &one, sizeof one, hipMemcpyHostToDevice));
+    a.gran = reinterpret_cast<unsigned long long*>(base + gran_off);
+    HIP_TRY(hipHostMalloc(&c->persist_err, sizeof(unsigned), hipHostMallocMapped));
+    *c->persist_err = 0;
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->persist_err_dev), c->persist_err, 0));
+    a.err = c->persist_err_dev;
+    c->persist_ready = true;
+    return 0;
+}
+
+// after a synchronised replay: a persistent step that gave up on a hand-off left wrong ids
+static int persist_check(l3_ctx* c) {
+    if (c->persist_err && *reinterpret_cast<volatile unsigned*>(c->persist_err))
+        return fail("persistent decode step: a workgroup timed out on an in-launch hand-off");
+    return 0;
+}
+
 // Capture `steps` consecutive decode steps (B sequences, L = 1), each reading its position from
 // dec_pos and its ids from dec_ids; each step's argmax writes the next ids back into dec_ids and
 // advances dec_pos, so the steps chain on the device.
 static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGraphExec_t* exec) {
     const bool timing = c->timing;
     c->timing = false;  // no event records inside the graph
+    const bool persist = persist_wanted(c, B);
+    if (persist && persist_setup(c)) { c->timing = timing; return 1; }
     HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc = 0;
     // batch 1: each step's argmax folded into the next step's layer-0 QKV, one argmax launch per
     // graph (its last step); the lm_heads move the position on
-    const int fold = fold_parts(c, B);
-    for (int i = 0; i < steps && !rc; ++i) {
+    const int fold = persist ? 0 : fold_parts(c, B);
+    for (int i = 0; i < steps && persist && !rc; ++i) {  // one launch per step
+        DecodePersistArgs a = c->persist;
+        a.ids = c->dec_ids;
+        a.st = c->dec_state;
+        a.kv_bak = c->bak_capture ? c->kv_bak : nullptr;
+        const hipError_t e = launch_decode_persist(a, c->stream);
+        if (e != hipSuccess) rc = fail("persistent decode step launch in capture failed: %s", hipGetErrorString(e));
+    }
+    for (int i = 0; i < steps && !persist && !rc; ++i) {
         c->fold_in = fold && i > 0;
         c->fold_adv = fold > 0;
         c->fold_n = fold;
@@ -1169,6 +1256,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
             if (!q.done) {
                 HIP_TRY(hipEventSynchronize(q.ev));
                 q.done = true;
+                if (persist_check(c)) return 1;
                 float ms = 0.f;  // the chunk's graph time on the device, per step
                 if (hipEventElapsedTime(&ms, q.ev0, q.ev1) == hipSuccess && ms > 0.f)
                     note_step_time(c, 1e3 * (double)ms / q.n);
@@ -1196,6 +1284,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
         HIP_TRY(hipGraphLaunch(c->dec_exec, c->stream));
         HIP_TRY(hipMemcpyAsync(c->dec_host, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if (persist_check(c)) return 1;
         note_step_time(c, now_us() - t0);
         for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
         c->dec_last.assign(next_ids_host, next_ids_host + B);
@@ -1308,6 +1397,7 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
     if (hipMemcpyAsync(all.data(), hist, all.size() * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return done(fail("generate: copy-back failed"));
+    if (persist_check(c)) return done(1);
     for (int i = 0; i < steps; ++i)
         for (int b = 0; b < B; ++b) out_ids_host[(size_t)b * steps + i] = all[(size_t)i * B + b];
     c->dec_last.assign(B, 0);
