@@ -203,6 +203,10 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     if (p.epoch[1]) return;
     __syncthreads();
     Ctx c{p, tag, pos, &bad_s, red_s};
+    auto stamp = [&](int k) {  // diagnostic timeline (DecodePersistArgs::stamps)
+        if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 64 + k] = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    };
+    stamp(0);
     const int64_t slab = (int64_t)qkvn + qdim + D + FD + D;
     u64* lm_g = p.gran + slab * p.n_layers;
     const int K4d = D / 4, K4f = FD / 4, K4q = qdim / 4;
@@ -275,6 +279,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                     *reinterpret_cast<float2*>(cache + coff) = float2{r0, r1};
                 }
             }
+            stamp(1 + 5 * li);
         }
         // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
         if (wg < H) {
@@ -360,6 +365,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 gput(g_o + qo + 4 * tid + 2, tag, o.z);
                 gput(g_o + qo + 4 * tid + 3, tag, o.w);
             }
+            stamp(2 + 5 * li);
         }
         // ---- stage C: O-proj + residual (llama3.py:211, 253) --------------------------------
         {
@@ -372,6 +378,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             float acc[1];
             dot_rows<1, NCD>(w, xs, K4q, acc);
             if (valid && tid % LPR == 0) gput(g_h1 + u, tag, hin[u] + acc[0]);
+            stamp(3 + 5 * li);
         }
         // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) -----------------------
         {
@@ -388,6 +395,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 const float g = acc[0] * rs, up = acc[1] * rs;
                 gput(g_hid + u, tag, g * __builtin_amdgcn_rcpf(1.0f + __expf(-g)) * up);
             }
+            stamp(4 + 5 * li);
         }
         // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
         {
@@ -400,6 +408,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             float acc[1];
             dot_rows<1, NCF>(w, xs, K4f, acc);
             if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);
+            stamp(5 + 5 * li);
         }
     }
     if (layer_wg) lm_load();  // in flight while the last layer's output arrives
@@ -414,6 +423,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             }
         }
         if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, layer_wg ? 1 : 8)) goto done;
+        stamp(60);
         const float rs = inv_rms(c, xs, D);
         float best = -INFINITY;
         int bi = 0x7fffffff;
@@ -445,6 +455,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             gput(lm_g + 2 * wg, tag, best);
             gput(lm_g + 2 * wg + 1, tag, __int_as_float(bi));
         }
+        stamp(61);
     }
     // ---- workgroup 0: the step's greedy id from the G partials; generate history, position ----
     if (wg == 0) {
@@ -471,6 +482,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 if (st->hist && q >= 0 && q < st->hist_cap) st->hist[q] = bi;
                 st->pos = pos + 1;
             }
+            stamp(62);
         }
     }
 done:

@@ -438,6 +438,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     for (hipEvent_t e : c->spec_free) (void)hipEventDestroy(e);
     dfree(c->spec_hist);
     dfree(c->persist_mem);
+    dfree(c->persist.stamps);
     if (c->persist_err) (void)hipHostFree(c->persist_err);
     if (c->spec_ids) (void)hipHostFree(c->spec_ids);
     if (c->hist_host) (void)hipHostFree(c->hist_host);
@@ -1007,8 +1008,25 @@ static int persist_setup(l3_ctx* c) {
     *c->persist_err = 0;
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->persist_err_dev), c->persist_err, 0));
     a.err = c->persist_err_dev;
+    // diagnostic timeline: L3_DECODE_PERSIST_STAMPS=<file> (tools/persist_stamps.py reads it; written
+    // at the end of every l3_greedy_generate_host)
+    if (getenv("L3_DECODE_PERSIST_STAMPS")) {
+        HIP_TRY(hipMalloc(&a.stamps, (size_t)256 * 64 * 8));
+        HIP_TRY(hipMemset(a.stamps, 0, (size_t)256 * 64 * 8));
+    }
     c->persist_ready = true;
     return 0;
+}
+
+static void persist_dump_stamps(l3_ctx* c) {
+    const char* path = getenv("L3_DECODE_PERSIST_STAMPS");
+    if (!path || !c->persist.stamps) return;
+    std::vector<unsigned long long> h((size_t)256 * 64);
+    if (hipMemcpy(h.data(), c->persist.stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    if (FILE* f = fopen(path, "wb")) {
+        fwrite(h.data(), 8, h.size(), f);
+        fclose(f);
+    }
 }
 
 // after a synchronised replay: a persistent step that gave up on a hand-off left wrong ids
@@ -1398,6 +1416,7 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
         hipStreamSynchronize(c->stream) != hipSuccess)
         return done(fail("generate: copy-back failed"));
     if (persist_check(c)) return done(1);
+    persist_dump_stamps(c);
     for (int i = 0; i < steps; ++i)
         for (int b = 0; b < B; ++b) out_ids_host[(size_t)b * steps + i] = all[(size_t)i * B + b];
     c->dec_last.assign(B, 0);
