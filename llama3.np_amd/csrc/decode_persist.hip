@@ -204,7 +204,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     __syncthreads();
     Ctx c{p, tag, pos, &bad_s, red_s};
     auto stamp = [&](int k) {  // diagnostic timeline (DecodePersistArgs::stamps)
-        if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 64 + k] = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 128 + k] = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     };
     stamp(0);
     const int64_t slab = (int64_t)qkvn + qdim + D + FD + D;
@@ -263,6 +263,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             } else if (!sweep_n(c, p.gran + slab * (li - 1) + qkvn + qdim + D + FD, D, hin, [](int i) { return i; })) {
                 goto done;
             }
+            stamp(1 + 10 * li);
             const float rs = inv_rms(c, hin, D);
             float acc[2];
             dot_rows<2, NCD>(w, hin, K4d, acc);
@@ -279,7 +280,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                     *reinterpret_cast<float2*>(cache + coff) = float2{r0, r1};
                 }
             }
-            stamp(1 + 5 * li);
+            stamp(2 + 10 * li);
         }
         // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
         if (wg < H) {
@@ -303,6 +304,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
             if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
                 goto done;
+            stamp(3 + 10 * li);
             const f32x4* q4 = reinterpret_cast<const f32x4*>(qs);
             const f32x4* kn4 = reinterpret_cast<const f32x4*>(qs + HD);
             const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
@@ -365,7 +367,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 gput(g_o + qo + 4 * tid + 2, tag, o.z);
                 gput(g_o + qo + 4 * tid + 3, tag, o.w);
             }
-            stamp(2 + 5 * li);
+            stamp(4 + 10 * li);
         }
         // ---- stage C: O-proj + residual (llama3.py:211, 253) --------------------------------
         {
@@ -375,10 +377,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             f32x4 w[1][NCD];
             load_rows<1, NCD>(p.wo[li], row, K4q, valid, w);
             if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
+            stamp(5 + 10 * li);
             float acc[1];
             dot_rows<1, NCD>(w, xs, K4q, acc);
             if (valid && tid % LPR == 0) gput(g_h1 + u, tag, hin[u] + acc[0]);
-            stamp(3 + 5 * li);
+            stamp(6 + 10 * li);
         }
         // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) -----------------------
         {
@@ -388,6 +391,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             f32x4 w[2][NCD];
             load_rows<2, NCD>(p.wgu[li], row, K4d, valid, w);
             if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
+            stamp(7 + 10 * li);
             const float rs = inv_rms(c, h1s, D);
             float acc[2];
             dot_rows<2, NCD>(w, h1s, K4d, acc);
@@ -395,7 +399,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 const float g = acc[0] * rs, up = acc[1] * rs;
                 gput(g_hid + u, tag, g * __builtin_amdgcn_rcpf(1.0f + __expf(-g)) * up);
             }
-            stamp(4 + 5 * li);
+            stamp(8 + 10 * li);
         }
         // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
         {
@@ -405,10 +409,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             f32x4 w[1][NCF];
             load_rows<1, NCF>(p.wd[li], row, K4f, valid, w);
             if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
+            stamp(9 + 10 * li);
             float acc[1];
             dot_rows<1, NCF>(w, xs, K4f, acc);
             if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);
-            stamp(5 + 5 * li);
+            stamp(10 + 10 * li);
         }
     }
     if (layer_wg) lm_load();  // in flight while the last layer's output arrives
@@ -423,8 +428,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             }
         }
         if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, layer_wg ? 1 : 8)) goto done;
-        stamp(60);
+        stamp(100);
         const float rs = inv_rms(c, xs, D);
+        stamp(103);
         float best = -INFINITY;
         int bi = 0x7fffffff;
         for (int ps = 0; ps < lm_passes; ++ps) {
@@ -444,6 +450,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const float v = acc[0] * rs;
             if (r < lm_r1 && argmax_better(v, r, best, bi)) { best = v; bi = r; }
         }
+        stamp(104);
         group_argmax<64>(best, bi, tid & 63);
         __shared__ float bv_s[4];
         __shared__ int bi_s[4];
@@ -455,12 +462,13 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             gput(lm_g + 2 * wg, tag, best);
             gput(lm_g + 2 * wg + 1, tag, __int_as_float(bi));
         }
-        stamp(61);
+        stamp(101);
     }
     // ---- workgroup 0: the step's greedy id from the G partials; generate history, position ----
     if (wg == 0) {
         float* pv = xs;  // [2G]
         if (sweep_n(c, lm_g, 2 * G, pv, [](int i) { return i; })) {
+            stamp(105);
             float best = -INFINITY;
             int bi = 0x7fffffff;
             for (int i = tid; i < G; i += NT)
@@ -482,7 +490,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 if (st->hist && q >= 0 && q < st->hist_cap) st->hist[q] = bi;
                 st->pos = pos + 1;
             }
-            stamp(62);
+            stamp(102);
         }
     }
 done:

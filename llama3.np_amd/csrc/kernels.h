@@ -260,7 +260,7 @@ struct DecodePersistArgs {
     unsigned long long* gran;      // granule slabs (decode_persist.hip), zeroed at allocation
     unsigned* epoch;               // [0] granule tag of the next launch (starts at 1); [1] sticky failure
     unsigned* err;                 // host-mapped: set to 1 when a workgroup gave up on a hand-off
-    unsigned long long* stamps;    // diagnostic (null): [workgroup][64] s_memtime after each stage
+    unsigned long long* stamps;    // diagnostic (null): [workgroup][128] s_memrealtime at stage points
 };
 bool decode_persist_ok(const DecodePersistArgs& a);
 hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s);

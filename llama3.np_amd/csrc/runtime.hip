@@ -1011,8 +1011,8 @@ static int persist_setup(l3_ctx* c) {
     // diagnostic timeline: L3_DECODE_PERSIST_STAMPS=<file> (tools/persist_stamps.py reads it; written
     // at the end of every l3_greedy_generate_host)
     if (getenv("L3_DECODE_PERSIST_STAMPS")) {
-        HIP_TRY(hipMalloc(&a.stamps, (size_t)256 * 64 * 8));
-        HIP_TRY(hipMemset(a.stamps, 0, (size_t)256 * 64 * 8));
+        HIP_TRY(hipMalloc(&a.stamps, (size_t)256 * 128 * 8));
+        HIP_TRY(hipMemset(a.stamps, 0, (size_t)256 * 128 * 8));
     }
     c->persist_ready = true;
     return 0;
@@ -1021,7 +1021,7 @@ static int persist_setup(l3_ctx* c) {
 static void persist_dump_stamps(l3_ctx* c) {
     const char* path = getenv("L3_DECODE_PERSIST_STAMPS");
     if (!path || !c->persist.stamps) return;
-    std::vector<unsigned long long> h((size_t)256 * 64);
+    std::vector<unsigned long long> h((size_t)256 * 128);
     if (hipMemcpy(h.data(), c->persist.stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
     if (FILE* f = fopen(path, "wb")) {
         fwrite(h.data(), 8, h.size(), f);

@@ -3,10 +3,9 @@
     L3_DECODE_PERSIST=1 L3_DECODE_PERSIST_STAMPS=gpurun_out/pstamps.bin python tools/persist_stamps.py
 
 Runs a 145-step greedy loop on stories15M-shaped synthetic weights (the library dumps the last
-step's stamps: [workgroup][64] s_memrealtime, 100 MHz), then prints when each stage ended
-relative to the launch's earliest stamp: stage k of layer l at slot 1 + 5 l + k (QKV, attention,
-O-proj, gate|up, down), 60 = the lm_head input arrived, 61 = lm_head partial published, 62 =
-greedy id written (workgroup 0)."""
+step's stamps: [workgroup][128] s_memrealtime, 100 MHz), then prints, per stage, when its input
+arrived (slot 1 + 10 l + 2 k) and its output was published (2 + 10 l + 2 k) relative to the
+launch's earliest stamp; 100-105 the lm_head and the final argmax."""
 import os
 import sys
 import tempfile
@@ -27,30 +26,30 @@ if "--read" not in sys.argv:
         synth.save_npz(p, w)
         m = llama3.Llama(p, args)
     m.generate_all(np.array([[1, 76, 505, 263, 12561]]), 150)
-st = np.fromfile(path, dtype=np.uint64).reshape(256, 64).astype(np.int64)
+st = np.fromfile(path, dtype=np.uint64).reshape(256, 128).astype(np.int64)
 t0 = st[:, 0][st[:, 0] > 0].min()
 us = lambda x: (x - t0) / 100.0  # noqa: E731
 names = ["qkv", "attn", "oproj", "gateup", "down"]
-print("workgroup 0 (a layer workgroup), stage ends in us from the launch's first stamp:")
-prev = 0.0
-for li in range(6):
-    row = []
-    for k in range(5):
-        v = st[0, 1 + 5 * li + k]
-        if v:
-            row.append(f"{names[k]} {us(v):6.2f} (+{us(v) - prev:5.2f})")
-            prev = us(v)
-    print(f"  layer {li}: " + "  ".join(row))
-for k, nm in ((60, "lm input"), (61, "lm partial"), (62, "greedy id")):
-    if st[0, k]:
-        print(f"  {nm}: {us(st[0, k]):6.2f}")
 lay = st[:64]
-for k in range(1, 31):
-    col = lay[:, k][lay[:, k] > 0]
-    if len(col):
-        print(f"  slot {k:2d} {names[(k - 1) % 5]:6s} layer {(k - 1) // 5}: first {us(col.min()):6.2f} last {us(col.max()):6.2f}")
-oth = st[64:]
-for k in (0, 60, 61):
-    col = oth[:, k][oth[:, k] > 0]
-    if len(col):
-        print(f"  lm workgroups slot {k}: first {us(col.min()):6.2f} last {us(col.max()):6.2f}")
+
+
+def span(rows, k):
+    col = rows[:, k][rows[:, k] > 0]
+    return (us(col.min()), us(col.max())) if len(col) else (None, None)
+
+
+print("layer workgroups: per stage, input arrived (first..last) -> output published (first..last), us")
+for li in range(6):
+    for k in range(5):
+        a0, a1 = span(lay, 1 + 10 * li + 2 * k)
+        p0, p1 = span(lay, 2 + 10 * li + 2 * k)
+        if p0 is None:
+            continue
+        arr = f"{a0:7.2f}..{a1:7.2f}" if a0 is not None else " " * 16
+        print(f"  L{li} {names[k]:6s} in {arr}  out {p0:7.2f}..{p1:7.2f}")
+for k, nm in ((0, "start"), (100, "lm input"), (103, "lm rms"), (104, "lm rows done"), (101, "lm partial")):
+    a = span(st[:64], k)
+    b = span(st[64:], k)
+    print(f"  {nm:12s} layer wgs {a[0]}..{a[1]}   lm wgs {b[0]}..{b[1]}")
+for k, nm in ((105, "wg0 partials in"), (102, "greedy id")):
+    print(f"  {nm}: {us(st[0, k]):.2f}")
