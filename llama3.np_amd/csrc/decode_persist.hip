@@ -74,11 +74,9 @@ __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, I
     for (unsigned spin = 0;; ++spin) {
         ok = true;
         u64 x[PER];
+        // unpredicated (a clamped index past n: a predicated load is a branch that waits)
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = tid + NT * k;
-            x[k] = i < n ? gget(g + idx(i)) : ((u64)c.tag << 32);
-        }
+        for (int k = 0; k < PER; ++k) x[k] = gget(g + idx(min(tid + NT * k, n - 1)));
 #pragma unroll
         for (int k = 0; k < PER; ++k) ok &= (unsigned)(x[k] >> 32) == c.tag;
         if (ok) {
@@ -89,7 +87,7 @@ __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, I
             }
             break;
         }
-        if (spin > (1u << 20) || *c.bad) {
+        if (spin > (1u << 20) || ((spin & 255) == 255 && *c.bad)) {  // another wave gave up
             give_up(c);
             break;
         }
@@ -133,18 +131,31 @@ __device__ __forceinline__ float inv_rms(const Ctx& c, const float* x, int n) {
     return __builtin_amdgcn_rsqf(s / (float)n + c.p.eps);
 }
 
-// W rows of one unit into registers: lane j of the unit holds float4s k4 = j + LPR * t, t < NC
+// global (not flat) 16-byte loads: flat loads also count in lgkmcnt, so every LDS wait would
+// wait for them too
+typedef const __attribute__((address_space(1))) f32x4* gf4p;
+__device__ __forceinline__ gf4p gf4(const void* p) { return (gf4p)(p); }
+
+// W rows of one unit into registers: lane j of the unit holds float4s k4 = j + LPR * t, t < NC.
+// Unpredicated loads from clamped (in-bounds) addresses, zeroed afterwards where they fall past
+// K or the unit is not valid: a predicated load compiles to an exec-masked branch that waits for
+// every load in flight before the next one is issued (one round trip per float4)
 template <int ROWS, int NC>
 __device__ __forceinline__ void load_rows(const float* W, const int (&row)[ROWS], int K4, bool valid,
                                           f32x4 (&w)[ROWS][NC]) {
     const int j = threadIdx.x % LPR;
-    const f32x4* W4 = reinterpret_cast<const f32x4*>(W);
+    const gf4p W4 = gf4(W);
 #pragma unroll
     for (int t = 0; t < NC; ++t) {
-        const int k4 = j + LPR * t;
+        const int k4 = j + LPR * t, kk = min(k4, K4 - 1);
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r)
-            w[r][t] = (valid && k4 < K4) ? W4[(int64_t)row[r] * K4 + k4] : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < ROWS; ++r) w[r][t] = W4[(int64_t)row[r] * K4 + kk];
+    }
+#pragma unroll
+    for (int t = 0; t < NC; ++t) {
+        const bool in = valid && j + LPR * t < K4;
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) w[r][t] = in ? w[r][t] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 }
 
@@ -291,15 +302,20 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const f32x4* V4p = reinterpret_cast<const f32x4*>(cv + (int64_t)kvh * p.Smax * HD);
             // keys before pos come from the cache (earlier launches); key pos from the granules
             constexpr int VPF = 8;
+            // unpredicated loads from clamped rows (see load_rows), zeroed where not used; row
+            // pos - 1 is the last one an earlier launch wrote (pos >= 1 in a decode step)
+            const int kmax = pos > 0 ? pos - 1 : 0;
+            const gf4p Kg = gf4(K4p), Vg = gf4(V4p);
             f32x4 kr[KPF];
 #pragma unroll
-            for (int i = 0; i < KPF; ++i) kr[i] = (i < D4 && tid < pos) ? K4p[(int64_t)tid * D4 + i] : f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
             f32x4 vr[VPF];
 #pragma unroll
-            for (int t = 0; t < VPF; ++t) {
-                const int k = rg + t * R;
-                vr[t] = (rg < R && k < pos) ? V4p[(int64_t)k * D4 + d4] : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + min(d4, D4 - 1)];
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) kr[i] = (i < D4 && tid < pos) ? kr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < VPF; ++t) vr[t] = (rg < R && rg + t * R < pos) ? vr[t] : f32x4{0.f, 0.f, 0.f, 0.f};
             float* qs = xs;                              // q | k_new | v_new of this head
             const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
             if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
