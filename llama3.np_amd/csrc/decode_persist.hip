@@ -159,20 +159,23 @@ __device__ __forceinline__ void load_rows(const float* W, const int (&row)[ROWS]
     }
 }
 
+// branch-free: every chunk's LDS read is issued before the first FMA (x read at a clamped index
+// past K meets a zeroed W chunk); a per-chunk bound check compiled to a branch and an LDS wait
+// per chunk (the lm_head's eight passes took 3 us)
 template <int ROWS, int NC>
 __device__ __forceinline__ void dot_rows(const f32x4 (&w)[ROWS][NC], const float* x, int K4, float (&acc)[ROWS]) {
     const int j = threadIdx.x % LPR;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(x);
+    f32x4 xv[NC];
+#pragma unroll
+    for (int t = 0; t < NC; ++t) xv[t] = X4[min(j + LPR * t, K4 - 1)];
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
 #pragma unroll
-    for (int t = 0; t < NC; ++t) {
-        const int k4 = j + LPR * t;
-        if (k4 >= K4) break;
-        const f32x4 xv = X4[k4];
+    for (int t = 0; t < NC; ++t)
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) acc[r] += w[r][t].x * xv.x + w[r][t].y * xv.y + w[r][t].z * xv.z + w[r][t].w * xv.w;
-    }
+        for (int r = 0; r < ROWS; ++r)
+            acc[r] += w[r][t].x * xv[t].x + w[r][t].y * xv[t].y + w[r][t].z * xv[t].z + w[r][t].w * xv[t].w;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) acc[r] = group_sum<LPR>(acc[r]);
 }
@@ -464,7 +467,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 dot_rows<1, NCD>(w, xs, K4d, acc);
             }
             const float v = acc[0] * rs;
-            if (r < lm_r1 && argmax_better(v, r, best, bi)) { best = v; bi = r; }
+            const bool take = r < lm_r1 && argmax_better(v, r, best, bi);
+            best = take ? v : best;
+            bi = take ? r : bi;
         }
         stamp(104);
         group_argmax<64>(best, bi, tid & 63);
