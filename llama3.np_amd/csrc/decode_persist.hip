@@ -226,9 +226,16 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     const int K4d = D / 4, K4f = FD / 4, K4q = qdim / 4;
     const bool layer_wg = wg < p.GL;
 
-    // lm_head rows of this workgroup: [r0, r1); unit = one row, LPR lanes
-    const int lm_per = (p.VS + G - 1) / G, lm_r0 = wg * lm_per, lm_r1 = min(p.VS, lm_r0 + lm_per);
-    const int lm_passes = (lm_r1 - lm_r0 + UPP - 1) / UPP;
+    // lm_head rows of this workgroup: [r0, r1); unit = one row, LPR lanes.  Only the workgroups
+    // past GL take rows: they load them at launch, while the layers run (rows on the layer
+    // workgroups were loaded after their last stage and made the final argmax wait ~1 us)
+    const int nlm = G - p.GL, lwg = wg - p.GL;
+    const int lm_per = (p.VS + nlm - 1) / nlm;
+    const int lm_r0 = lwg < 0 ? p.VS : lwg * lm_per, lm_r1 = min(p.VS, lm_r0 + lm_per);
+    const int lm_passes = lm_r1 > lm_r0 ? (lm_r1 - lm_r0 + UPP - 1) / UPP : 0;
+    // the generate-history fields workgroup 0 writes at the end, fetched now (off the final path)
+    const int hist_base = p.st->hist_base, hist_cap = p.st->hist_cap;
+    int32_t* const hist = p.st->hist;
     f32x4 lw[LMPF][1][NCD];
     auto lm_load = [&]() {
 #pragma unroll
@@ -379,6 +386,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             __syncthreads();
             if (tid < D4) {
                 f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
                 for (int r = 0; r < R; ++r) o += part[r * D4 + tid];
                 o *= 1.0f / l;
                 gput(g_o + qo + 4 * tid + 0, tag, o.x);
@@ -435,41 +443,46 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             stamp(10 + 10 * li);
         }
     }
-    if (layer_wg) lm_load();  // in flight while the last layer's output arrives
+    if (layer_wg) {
+        if (wg == 0) goto final;  // the final argmax; the other layer workgroups are done
+        goto done;
+    }
 
     // ---- final RMSNorm + lm_head (llama3.py:304-307) + this workgroup's argmax (:320) ---------
     {
         u64* g_last = p.gran + slab * (p.n_layers - 1) + qkvn + qdim + D + FD;
-        if (!layer_wg && tid == 0) {  // a long wait: one lane polls the last granule, sleeping
+        if (tid == 0) {  // a long wait: one lane polls the last granule, sleeping
             for (unsigned spin = 0; (unsigned)(gget(g_last + D - 1) >> 32) != tag; ++spin) {
                 if (spin > (1u << 20)) break;
                 __builtin_amdgcn_s_sleep(16);
             }
         }
-        if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, layer_wg ? 1 : 8)) goto done;
+        if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, 8)) goto done;
         stamp(100);
         const float rs = inv_rms(c, xs, D);
         stamp(103);
         float best = -INFINITY;
         int bi = 0x7fffffff;
-        for (int ps = 0; ps < lm_passes; ++ps) {
-            const int r = lm_r0 + ps * UPP + tid / LPR;
-            float acc[1];
-            if (ps < LMPF) {
-                // a compile-time index into lw: unrolled select
-#pragma unroll
-                for (int q = 0; q < LMPF; ++q)
-                    if (q == ps) dot_rows<1, NCD>(lw[q], xs, K4d, acc);
-            } else {
-                f32x4 w[1][NCD];
-                const int row[1] = {min(r, p.VS - 1)};
-                load_rows<1, NCD>(p.lm_head, row, K4d, r < lm_r1, w);
-                dot_rows<1, NCD>(w, xs, K4d, acc);
-            }
-            const float v = acc[0] * rs;
+        auto consider = [&](int r, float dot) {
+            const float v = dot * rs;
             const bool take = r < lm_r1 && argmax_better(v, r, best, bi);
             best = take ? v : best;
             bi = take ? r : bi;
+        };
+#pragma unroll
+        for (int ps = 0; ps < LMPF; ++ps) {  // the passes held in registers since the launch
+            float acc[1];
+            dot_rows<1, NCD>(lw[ps], xs, K4d, acc);
+            consider(lm_r0 + ps * UPP + tid / LPR, acc[0]);
+        }
+        for (int ps = LMPF; ps < lm_passes; ++ps) {  // rows past them, streamed now
+            const int r = lm_r0 + ps * UPP + tid / LPR;
+            f32x4 w[1][NCD];
+            const int row[1] = {min(r, p.VS - 1)};
+            load_rows<1, NCD>(p.lm_head, row, K4d, r < lm_r1, w);
+            float acc[1];
+            dot_rows<1, NCD>(w, xs, K4d, acc);
+            consider(r, acc[0]);
         }
         stamp(104);
         group_argmax<64>(best, bi, tid & 63);
@@ -480,23 +493,27 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         if (tid == 0) {
             for (int w2 = 1; w2 < 4; ++w2)
                 if (argmax_better(bv_s[w2], bi_s[w2], best, bi)) { best = bv_s[w2]; bi = bi_s[w2]; }
-            gput(lm_g + 2 * wg, tag, best);
-            gput(lm_g + 2 * wg + 1, tag, __int_as_float(bi));
+            gput(lm_g + 2 * lwg, tag, best);
+            gput(lm_g + 2 * lwg + 1, tag, __int_as_float(bi));
         }
         stamp(101);
+        goto done;
     }
-    // ---- workgroup 0: the step's greedy id from the G partials; generate history, position ----
-    if (wg == 0) {
-        float* pv = xs;  // [2G]
-        if (sweep_n(c, lm_g, 2 * G, pv, [](int i) { return i; })) {
+final:
+    // ---- workgroup 0: the step's greedy id from the lm partials; generate history, position ----
+    {
+        float* pv = xs;  // [2 nlm]
+        if (sweep_n(c, lm_g, 2 * nlm, pv, [](int i) { return i; })) {
             stamp(105);
             float best = -INFINITY;
             int bi = 0x7fffffff;
-            for (int i = tid; i < G; i += NT)
-                if (argmax_better(pv[2 * i], __float_as_int(pv[2 * i + 1]), best, bi)) {
-                    best = pv[2 * i];
-                    bi = __float_as_int(pv[2 * i + 1]);
-                }
+            for (int i = tid; i < nlm; i += NT) {
+                const float v = pv[2 * i];
+                const int ix = __float_as_int(pv[2 * i + 1]);
+                const bool take = argmax_better(v, ix, best, bi);
+                best = take ? v : best;
+                bi = take ? ix : bi;
+            }
             group_argmax<64>(best, bi, tid & 63);
             __shared__ float fb[4];
             __shared__ int fi[4];
@@ -506,10 +523,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 for (int w2 = 1; w2 < 4; ++w2)
                     if (argmax_better(fb[w2], fi[w2], best, bi)) { best = fb[w2]; bi = fi[w2]; }
                 p.ids[0] = bi;
-                DecState* st = p.st;
-                const int q = pos - st->hist_base;
-                if (st->hist && q >= 0 && q < st->hist_cap) st->hist[q] = bi;
-                st->pos = pos + 1;
+                const int q = pos - hist_base;
+                if (hist && q >= 0 && q < hist_cap) hist[q] = bi;
+                p.st->pos = pos + 1;
             }
             stamp(102);
         }
@@ -528,7 +544,7 @@ bool decode_persist_ok(const DecodePersistArgs& a) {
            a.H % a.KVH == 0 && a.H * a.HD == a.D && ncd_of(a.D) && ncf_of(a.FD) && qkvn % 2 == 0 &&
            (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD + a.GL - 1) / a.GL <= persist::UPP &&
            (a.D + a.GL - 1) / a.GL <= persist::UPP && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
-           a.n_layers >= 1 && a.GL >= 1 && a.GL <= 256;
+           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256;
 }
 
 // Grid of one decode step: one workgroup per CU (256 on MI355X; every one resident: 1 per CU by
@@ -540,7 +556,7 @@ hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return hipErrorNotSupported;
     const int grid = cus < 256 ? cus : 256;
-    if (grid < a.GL) return hipErrorNotSupported;
+    if (grid <= a.GL || 2 * (grid - a.GL) > a.Xp) return hipErrorNotSupported;
     const size_t lds = ((size_t)2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
     const int ncd = ncd_of(a.D), ncf = ncf_of(a.FD);
 #define L3_PERSIST(NCD, NCF, KPF, LMPF)                                                            \
@@ -549,7 +565,7 @@ hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s) {
         return hipGetLastError();                                                                  \
     }
     L3_PERSIST(1, 3, 16, 8)   // tiny models (tests)
-    L3_PERSIST(5, 12, 12, 8)  // stories15M: D 288, FD 768, HD 48
+    L3_PERSIST(5, 12, 12, 11)  // stories15M: D 288, FD 768, HD 48 (167 lm rows per lm workgroup)
     L3_PERSIST(5, 16, 16, 4)
     L3_PERSIST(8, 16, 16, 2)
     L3_PERSIST(1, 12, 16, 8)
