@@ -362,7 +362,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 sc[k] = s;
                 m = fmaxf(m, s);
             }
+            if (li == 1) stamp(110);
             m = block_max(c, m);
+            if (li == 1) stamp(111);
             float l = 0.f;
             for (int k = tid; k < S; k += NT) {
                 const float e = __builtin_amdgcn_exp2f(sc[k] - m);  // q carries log2(e) / sqrt(HD)
@@ -370,6 +372,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 l += e;
             }
             l = block_sum(c, l);  // its barriers also publish sc
+            if (li == 1) stamp(112);
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             if (rg < R) {
 #pragma unroll
@@ -380,10 +383,12 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
                 if (pos % R == rg) acc += sc[pos] * vn4[d4];
             }
-            __syncthreads();  // xs (q) may be reused as the reduction buffer below
+            if (li == 1) stamp(113);
+            __syncthreads();
             f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
             if (rg < R) part[rg * D4 + d4] = acc;
             __syncthreads();
+            if (li == 1) stamp(114);
             if (tid < D4) {
                 f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll 8
