@@ -50,6 +50,16 @@ __device__ __forceinline__ u64 gget(u64* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup barrier for LDS traffic only: __syncthreads() is also a workgroup-scope release of
+// global memory, i.e. an s_waitcnt vmcnt(0) that waits for this wave's write-through granule /
+// cache / stamp stores to be acknowledged (~1 us) before the barrier.  Nothing in this kernel
+// reads through global memory what another wave of its own workgroup wrote in the same launch,
+// so the stage-internal barriers only need the LDS writes done (asm: the compiler neither moves
+// memory accesses across it nor sees a barrier it would pad with waits).
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 struct Ctx {
     const DecodePersistArgs& p;
     unsigned tag;
@@ -94,7 +104,7 @@ __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, I
         if (sleep == 1) __builtin_amdgcn_s_sleep(1);
         else __builtin_amdgcn_s_sleep(8);
     }
-    __syncthreads();
+    lds_barrier();
     return !*c.bad;
 }
 
@@ -109,17 +119,17 @@ __device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst,
 __device__ __forceinline__ float block_sum(const Ctx& c, float v) {
     v = group_sum<64>(v);
     const int tid = threadIdx.x;
-    __syncthreads();
+    lds_barrier();
     if ((tid & 63) == 0) c.red[tid >> 6] = v;
-    __syncthreads();
+    lds_barrier();
     return (c.red[0] + c.red[1]) + (c.red[2] + c.red[3]);
 }
 __device__ __forceinline__ float block_max(const Ctx& c, float v) {
     v = group_max<64>(v);
     const int tid = threadIdx.x;
-    __syncthreads();
+    lds_barrier();
     if ((tid & 63) == 0) c.red[tid >> 6] = v;
-    __syncthreads();
+    lds_barrier();
     return fmaxf(fmaxf(c.red[0], c.red[1]), fmaxf(c.red[2], c.red[3]));
 }
 
@@ -215,7 +225,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     const int id = p.ids[0];
     // an earlier launch gave up (epoch[1], sticky): do nothing, the host reports it
     if (p.epoch[1]) return;
-    __syncthreads();
+    lds_barrier();
     Ctx c{p, tag, pos, &bad_s, red_s};
     auto stamp = [&](int k) {  // diagnostic timeline (DecodePersistArgs::stamps)
         if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 128 + k] = __builtin_amdgcn_s_memrealtime();  // 100 MHz
@@ -280,7 +290,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             // layer's output granules
             if (li == 0) {
                 for (int i = tid; i < D; i += NT) hin[i] = p.emb[(int64_t)id * D + i];
-                __syncthreads();
+                lds_barrier();
             } else if (!sweep_n(c, p.gran + slab * (li - 1) + qkvn + qdim + D + FD, D, hin, [](int i) { return i; })) {
                 goto done;
             }
@@ -384,10 +394,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 if (pos % R == rg) acc += sc[pos] * vn4[d4];
             }
             if (li == 1) stamp(113);
-            __syncthreads();
             f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
             if (rg < R) part[rg * D4 + d4] = acc;
-            __syncthreads();
+            lds_barrier();
             if (li == 1) stamp(114);
             if (tid < D4) {
                 f32x4 o = {0.f, 0.f, 0.f, 0.f};
@@ -494,7 +503,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         __shared__ float bv_s[4];
         __shared__ int bi_s[4];
         if ((tid & 63) == 0) { bv_s[tid >> 6] = best; bi_s[tid >> 6] = bi; }
-        __syncthreads();
+        lds_barrier();
         if (tid == 0) {
             for (int w2 = 1; w2 < 4; ++w2)
                 if (argmax_better(bv_s[w2], bi_s[w2], best, bi)) { best = bv_s[w2]; bi = bi_s[w2]; }
@@ -523,7 +532,7 @@ final:
             __shared__ float fb[4];
             __shared__ int fi[4];
             if ((tid & 63) == 0) { fb[tid >> 6] = best; fi[tid >> 6] = bi; }
-            __syncthreads();
+            lds_barrier();
             if (tid == 0) {
                 for (int w2 = 1; w2 < 4; ++w2)
                     if (argmax_better(fb[w2], fi[w2], best, bi)) { best = fb[w2]; bi = fi[w2]; }
