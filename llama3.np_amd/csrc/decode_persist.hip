@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     if (tid == 0) bad_s = 0;
     const unsigned tag = p.epoch[0];
     const int pos = p.st->pos;
-    const int id = p.ids[0];
+    int id = p.ids[0];
     // an earlier launch gave up (epoch[1], sticky): do nothing, the host reports it
     if (p.epoch[1]) return;
     lds_barrier();
@@ -256,6 +256,41 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         }
     };
     if (!layer_wg) lm_load();  // nothing else to do: the rows land while the layers run
+
+    // from_parts: the previous step (the launch before this one in the same graph) left its
+    // lm_head partials and no id; every layer workgroup reduces them itself (plain loads: written
+    // by the previous launch) — its final argmax hand-off and reduction come off that step's tail.
+    // This launch's own partials overwrite them only after every layer workgroup has started
+    // (the lm stage waits for the whole layer chain, which needs every layer workgroup).
+    if (p.from_parts && layer_wg) {
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < nlm; i += NT) {
+            const u64 v = lm_g[2 * i], x = lm_g[2 * i + 1];
+            const float bv = __uint_as_float((unsigned)v);
+            const int ix = (int)(unsigned)x;
+            const bool take = argmax_better(bv, ix, best, bi);
+            best = take ? bv : best;
+            bi = take ? ix : bi;
+        }
+        group_argmax<64>(best, bi, tid & 63);
+        __shared__ float pb[4];
+        __shared__ int pi[4];
+        if ((tid & 63) == 0) { pb[tid >> 6] = best; pi[tid >> 6] = bi; }
+        lds_barrier();
+        best = pb[0];
+        bi = pi[0];
+        for (int w2 = 1; w2 < 4; ++w2) {
+            const bool take = argmax_better(pb[w2], pi[w2], best, bi);
+            best = take ? pb[w2] : best;
+            bi = take ? pi[w2] : bi;
+        }
+        id = bi;
+        if (wg == 0 && tid == 0) {  // the previous step's id: its generate history entry
+            const int q = pos - 1 - hist_base;
+            if (hist && q >= 0 && q < hist_cap) hist[q] = id;
+        }
+    }
 
     for (int li = 0; li < p.n_layers && layer_wg; ++li) {
         u64* g_qkv = p.gran + slab * li;
@@ -458,7 +493,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         }
     }
     if (layer_wg) {
-        if (wg == 0) goto final;  // the final argmax; the other layer workgroups are done
+        if (wg != 0) goto done;
+        if (p.write_id) goto final;  // the final argmax (the last step of a graph)
+        // the next launch reduces this step's partials itself; only the position moves on here
+        // (every layer workgroup read it at its start: none could have finished layer 0 else)
+        if (tid == 0) p.st->pos = pos + 1;
         goto done;
     }
 

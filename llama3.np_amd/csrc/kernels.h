@@ -256,6 +256,9 @@ struct DecodePersistArgs {
     float* kv_bak;                 // null, or the run-ahead undo slots (GemmArgs::kv_bak layout, B = 1)
     int64_t bak_layer;             // floats per layer of kv_bak
     int32_t* ids;                  // [1]: this step's token id in, the next step's out
+    int from_parts;                // 1: the token id is the argmax of the previous launch's lm partials
+    int write_id;                  // 1: reduce this launch's partials to ids[0] / history (last step
+                                   //    of a graph); 0: leave them for the next launch
     DecState* st;                  // pos (read; +1), generate history
     unsigned long long* gran;      // granule slabs (decode_persist.hip), zeroed at allocation
     unsigned* epoch;               // [0] granule tag of the next launch (starts at 1); [1] sticky failure

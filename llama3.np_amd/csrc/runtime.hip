@@ -1054,6 +1054,8 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
         a.ids = c->dec_ids;
         a.st = c->dec_state;
         a.kv_bak = c->bak_capture ? c->kv_bak : nullptr;
+        a.from_parts = i > 0;            // the previous step in this graph left partials only
+        a.write_id = i == steps - 1;     // the last one publishes the id for the host / next graph
         const hipError_t e = launch_decode_persist(a, c->stream);
         if (e != hipSuccess) rc = fail("persistent decode step launch in capture failed: %s", hipGetErrorString(e));
     }
