@@ -198,6 +198,10 @@ int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
  * served by a captured-graph replay, and of those the ones a speculative step (launched when
  * the previous l3_greedy_step_host returned) answered. */
 int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits);
+/* Whether the captured batch-1 decode step is the persistent kernel (one launch per greedy step,
+ * decode_persist.hip: every layer, the lm_head and the argmax with in-launch hand-offs) rather
+ * than the 25-kernel graph; env L3_DECODE_PERSIST (read at capture) picks it. */
+int l3_decode_persistent(l3_ctx* ctx, int32_t* active);
 /* Lazy greedy decode runs up to 16 steps ahead of the caller on the device (undone if the
  * caller leaves the schedule, so results are unchanged), and at most ~4 ms of decode work by
  * the measured step time: a caller that stops early (EOS, an abandoned generator) or makes any

@@ -210,6 +210,7 @@ struct l3_ctx {
     unsigned* persist_err_dev = nullptr;
     DecodePersistArgs persist{};
     bool persist_ready = false;
+    bool persist_graph = false;      // the captured single-step graph runs the persistent step
 };
 
 // ---------------------------------------------------------------------------------------
@@ -954,7 +955,8 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
 // Persistent batch-1 decode step (decode_persist.hip): L3_DECODE_PERSIST=1 (A/B) and a shape the
 // kernel takes (decode_persist_ok).  Its buffers are made once, with the stream idle.
 static bool persist_wanted(l3_ctx* c, int B) {
-    static const bool on = env_knob("L3_DECODE_PERSIST", 0) != 0;
+    // read at every capture (captures are rare), so a process can A/B both paths
+    const bool on = env_knob("L3_DECODE_PERSIST", 0) != 0;
     if (!on || B != 1 || c->layers.empty() || !c->dec_state) return false;
     if (c->persist_ready) return true;
     DecodePersistArgs a{};
@@ -1137,6 +1139,7 @@ static int capture_decode_graph(l3_ctx* c, int B) {
     if (rc) return 1;
     c->dec_B = B;
     c->dec_bak = bak;
+    c->persist_graph = persist_wanted(c, B);
     return 0;
 }
 
@@ -1691,6 +1694,12 @@ extern "C" int l3_kernel_timing(l3_ctx* c, int32_t enable) {
 extern "C" int l3_set_decode_horizon(l3_ctx* c, int32_t end_pos) {
     CHECK_CTX(c);
     c->spec_limit = end_pos > 0 ? end_pos : 0x7fffffff;
+    return 0;
+}
+
+extern "C" int l3_decode_persistent(l3_ctx* c, int32_t* active) {
+    CHECK_CTX(c);
+    if (active) *active = c->dec_exec && c->persist_graph ? 1 : 0;
     return 0;
 }
 

@@ -79,6 +79,7 @@ _SIGNATURES = {
     "l3_kernel_timing": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
     "l3_decode_stats": (ctypes.c_int, [_P, _P, _P]),
+    "l3_decode_persistent": (ctypes.c_int, [_P, _P]),
     "l3_set_decode_horizon": (ctypes.c_int, [_P, _I32]),
     "l3_comm_unique_id": (ctypes.c_int, [_P]),
     "l3_comm_init": (ctypes.c_int, [_P, _I32, _I32, _P]),
@@ -368,6 +369,12 @@ class Context:
     def set_decode_horizon(self, end_pos: int) -> None:
         """Lazy decode runs ahead of the caller on the device; never at positions >= end_pos."""
         check(lib().l3_set_decode_horizon(self._h, int(end_pos)))
+
+    def decode_persistent(self) -> bool:
+        """True when the captured batch-1 decode step is the persistent one-launch kernel."""
+        v = ctypes.c_int32(0)
+        check(lib().l3_decode_persistent(self._h, ctypes.byref(v)))
+        return bool(v.value)
 
     def decode_stats(self) -> dict:
         """Decode steps served by graph replay, and of those by a speculative step."""

@@ -1132,3 +1132,33 @@ def test_c5_full_depth_full_size_rows_match_b1():
         errs[r] = float(np.max(np.abs(one.astype(np.float64) - out[r:r + 1])))
         np.testing.assert_allclose(one, out[r:r + 1], rtol=1e-5, atol=1e-5)
     print(f"c5 32 layers B=64 L=2048: rows vs B=1 max-abs {errs}, |logits| <= {float(np.abs(out).max()):.2f}")
+
+
+@pytest.mark.parametrize("preset", ["default", "sharp"])
+def test_persistent_decode_step_matches_golden(tmpdir_mod, monkeypatch, preset):
+    """The persistent batch-1 decode step (decode_persist.hip: one launch per greedy step, every
+    layer / the lm_head / the argmax with in-launch granule hand-offs; L3_DECODE_PERSIST=1)
+    against the reference's own 145 greedy ids of "I have a dream" (llama3.py:310-321, the
+    decode hole included): the device loop (8-step graphs, the inner steps leaving their argmax to
+    the next launch), the lazy generator with run-ahead, and a second generate on the caches the
+    first left behind, each bit-exact; and the graph path (L3_DECODE_PERSIST=0) still taken."""
+    g = load_golden(f"stories15m_{preset}")
+    args = synth.stories15m(1)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, int(g["seed"]), preset)
+    prompt = np.asarray(g["dream_prompt"]).reshape(1, -1)
+    want = np.asarray(g["dream_ids"]).reshape(1, -1)
+    n = int(g["dream_max_new"])
+    for on in ("1", "0"):
+        monkeypatch.setenv("L3_DECODE_PERSIST", on)
+        m = llama3.Llama(path, args)
+        np.testing.assert_array_equal(m.generate_all(prompt, n), want)
+        assert m.context.decode_persistent() == (on == "1")
+        lazy = np.concatenate(list(m.generate(prompt, n)), axis=1)
+        np.testing.assert_array_equal(lazy, want)
+        # an abandoned generator (run-ahead steps undone), then a full one
+        gen = m.generate(prompt, n)
+        for _ in range(20):
+            next(gen)
+        del gen
+        np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
+        assert m.context.decode_stats()["graph_steps"] > 0

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 L3_DECODE_PERSIST=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -rf \
-  -k "greedy or generate or speculative or run_ahead or tiny or cli or argmax_ties or cache_edges or ragged or last_layer" \
+  -k "persistent or greedy or generate or speculative or run_ahead or tiny or cli or argmax_ties or cache_edges or ragged or last_layer" \
   --timeout 300 --timeout-method thread > gpurun_out/persist_tests.log 2>&1
 rc=$?; echo "persist tests rc=$rc"; tail -5 gpurun_out/persist_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
