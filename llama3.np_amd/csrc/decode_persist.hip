@@ -202,8 +202,8 @@ __device__ __forceinline__ int stage_unit(const DecodePersistArgs& p, int n, int
 
 }  // namespace persist
 
-// One launch = one decode step.  Granule slab per layer: [qkv | o | h1 | hid | h2], then the
-// lm_head partials [2 * gridDim.x].
+// One launch = one decode step.  Granule slab per layer: [qkv | O-proj partials H x D | hid | h2]
+// (decode_persist_slab), then the lm_head partials [2 * gridDim.x].
 // NCD / NCF: float4 per lane of a W row with K = D / K = FD (>= ceil(K / 64)); KPF >= HD / 4; LMPF:
 // lm_head passes of 16 rows each workgroup holds in registers
 template <int NCD, int NCF, int KPF, int LMPF>
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     const int qdim = H * HD, kvdim = KVH * HD, qkvn = qdim + 2 * kvdim;
     float* hin = sm;              // [D]  layer input (residual of the O-proj)
     float* h1s = hin + p.Dp;      // [D]  FFN input (residual of the down-proj)
-    float* xs = h1s + p.Dp;       // [max(qkvn, FD, qdim)] stage input
+    float* xs = h1s + p.Dp;       // [max(qkvn, FD, H D)] stage input
     float* sc = xs + p.Xp;        // [Smax] attention scores
     const int tid = threadIdx.x, wg = blockIdx.x, G = gridDim.x;
     if (tid == 0) bad_s = 0;
@@ -231,7 +231,8 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 128 + k] = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     };
     stamp(0);
-    const int64_t slab = (int64_t)qkvn + qdim + D + FD + D;
+    const int64_t slab = decode_persist_slab(H, KVH, HD, D, FD);
+    const int64_t h2_off = (int64_t)qkvn + (int64_t)H * D + FD;  // h2 within a slab
     u64* lm_g = p.gran + slab * p.n_layers;
     const int K4d = D / 4, K4f = FD / 4, K4q = qdim / 4;
     const bool layer_wg = wg < p.GL;
@@ -246,264 +247,16 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     // the generate-history fields workgroup 0 writes at the end, fetched now (off the final path)
     const int hist_base = p.st->hist_base, hist_cap = p.st->hist_cap;
     int32_t* const hist = p.st->hist;
-    f32x4 lw[LMPF][1][NCD];
-    auto lm_load = [&]() {
+    if (!layer_wg) {
+        // ---- final RMSNorm + lm_head (llama3.py:304-307) + this workgroup's argmax (:320) ---------
+        f32x4 lw[LMPF][1][NCD];  // live on this path only (not across the layer loop)
 #pragma unroll
-        for (int ps = 0; ps < LMPF; ++ps) {
+        for (int ps = 0; ps < LMPF; ++ps) {  // nothing else to do: the rows land while the layers run
             const int r = lm_r0 + ps * UPP + tid / LPR;
             const int row[1] = {min(r, p.VS - 1)};
             load_rows<1, NCD>(p.lm_head, row, K4d, ps < lm_passes && r < lm_r1, lw[ps]);
         }
-    };
-    if (!layer_wg) lm_load();  // nothing else to do: the rows land while the layers run
-
-    // from_parts: the previous step (the launch before this one in the same graph) left its
-    // lm_head partials and no id; every layer workgroup reduces them itself (plain loads: written
-    // by the previous launch) — its final argmax hand-off and reduction come off that step's tail.
-    // This launch's own partials overwrite them only after every layer workgroup has started
-    // (the lm stage waits for the whole layer chain, which needs every layer workgroup).
-    if (p.from_parts && layer_wg) {
-        float best = -INFINITY;
-        int bi = 0x7fffffff;
-        for (int i = tid; i < nlm; i += NT) {
-            const u64 v = lm_g[2 * i], x = lm_g[2 * i + 1];
-            const float bv = __uint_as_float((unsigned)v);
-            const int ix = (int)(unsigned)x;
-            const bool take = argmax_better(bv, ix, best, bi);
-            best = take ? bv : best;
-            bi = take ? ix : bi;
-        }
-        group_argmax<64>(best, bi, tid & 63);
-        __shared__ float pb[4];
-        __shared__ int pi[4];
-        if ((tid & 63) == 0) { pb[tid >> 6] = best; pi[tid >> 6] = bi; }
-        lds_barrier();
-        best = pb[0];
-        bi = pi[0];
-        for (int w2 = 1; w2 < 4; ++w2) {
-            const bool take = argmax_better(pb[w2], pi[w2], best, bi);
-            best = take ? pb[w2] : best;
-            bi = take ? pi[w2] : bi;
-        }
-        id = bi;
-        if (wg == 0 && tid == 0) {  // the previous step's id: its generate history entry
-            const int q = pos - 1 - hist_base;
-            if (hist && q >= 0 && q < hist_cap) hist[q] = id;
-        }
-    }
-
-    for (int li = 0; li < p.n_layers && layer_wg; ++li) {
-        u64* g_qkv = p.gran + slab * li;
-        u64* g_o = g_qkv + qkvn;
-        u64* g_h1 = g_o + qdim;
-        u64* g_hid = g_h1 + D;
-        u64* g_h2 = g_hid + FD;
-        const float* wqkv = p.wqkv[li];
-        float* ck = p.cache_k[li];
-        float* cv = p.cache_v[li];
-        // ---- stage A: RMSNorm + QKV + RoPE + KV append (llama3.py:248, 166-185) -------------
-        {
-            bool valid;
-            const int u = stage_unit(p, qkvn / 2, wg, valid);  // RoPE pair (rows 2u, 2u + 1)
-            const int row[2] = {2 * u, 2 * u + 1};
-            f32x4 w[2][NCD];
-            load_rows<2, NCD>(wqkv, row, K4d, valid, w);
-            const int col = 2 * u;
-            const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
-            const int cc = col - (sec == 0 ? 0 : sec == 1 ? qdim : qdim + kvdim);
-            const int head = cc / HD, d = cc - head * HD;
-            float2 cs = {1.f, 0.f};
-            if (sec < 2) {
-                const int t = pos * (HD >> 1) + (d >> 1);
-                cs = float2{p.rope_cos[t], p.rope_sin[t]};
-            }
-            float* cache = sec == 1 ? ck : cv;
-            const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
-            float2 old = {0.f, 0.f};
-            if (p.kv_bak && sec > 0 && valid) old = *reinterpret_cast<const float2*>(cache + coff);
-            // the layer input: the token's embedding row (llama3.py:287), else the previous
-            // layer's output granules
-            if (li == 0) {
-                for (int i = tid; i < D; i += NT) hin[i] = p.emb[(int64_t)id * D + i];
-                lds_barrier();
-            } else if (!sweep_n(c, p.gran + slab * (li - 1) + qkvn + qdim + D + FD, D, hin, [](int i) { return i; })) {
-                goto done;
-            }
-            stamp(1 + 10 * li);
-            const float rs = inv_rms(c, hin, D);
-            float acc[2];
-            dot_rows<2, NCD>(w, hin, K4d, acc);
-            if (valid && tid % LPR == 0) {
-                const float v0 = acc[0] * rs, v1 = acc[1] * rs;
-                const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
-                const float s = sec == 0 ? p.q_scale : 1.0f;
-                gput(g_qkv + col, tag, r0 * s);
-                gput(g_qkv + col + 1, tag, r1 * s);
-                if (sec > 0) {
-                    if (p.kv_bak)  // [pos % KV_BAK_SLOTS][k, v][1][KVH][HD]: the slot it overwrites
-                        *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer +
-                                                   (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d) = old;
-                    *reinterpret_cast<float2*>(cache + coff) = float2{r0, r1};
-                }
-            }
-            stamp(2 + 10 * li);
-        }
-        // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
-        if (wg < H) {
-            const int h = wg, kvh = h / (H / KVH);
-            const int D4 = HD / 4, R = NT / D4;          // PV: R key groups x D4 float4 columns
-            const int rg = tid / D4, d4 = tid - rg * D4;
-            const f32x4* K4p = reinterpret_cast<const f32x4*>(ck + (int64_t)kvh * p.Smax * HD);
-            const f32x4* V4p = reinterpret_cast<const f32x4*>(cv + (int64_t)kvh * p.Smax * HD);
-            // keys before pos come from the cache (earlier launches); key pos from the granules
-            constexpr int VPF = 8;
-            // unpredicated loads from clamped rows (see load_rows), zeroed where not used; row
-            // pos - 1 is the last one an earlier launch wrote (pos >= 1 in a decode step)
-            const int kmax = pos > 0 ? pos - 1 : 0;
-            const gf4p Kg = gf4(K4p), Vg = gf4(V4p);
-            f32x4 kr[KPF];
-#pragma unroll
-            for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
-            f32x4 vr[VPF];
-#pragma unroll
-            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + min(d4, D4 - 1)];
-#pragma unroll
-            for (int i = 0; i < KPF; ++i) kr[i] = (i < D4 && tid < pos) ? kr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int t = 0; t < VPF; ++t) vr[t] = (rg < R && rg + t * R < pos) ? vr[t] : f32x4{0.f, 0.f, 0.f, 0.f};
-            float* qs = xs;                              // q | k_new | v_new of this head
-            const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
-            if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
-                goto done;
-            stamp(3 + 10 * li);
-            const f32x4* q4 = reinterpret_cast<const f32x4*>(qs);
-            const f32x4* kn4 = reinterpret_cast<const f32x4*>(qs + HD);
-            const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
-            const int S = pos + 1;
-            // key tid from the prefetched row (rows past HD are zero: the q4 reads past HD land
-            // in the k / v part of qs and add nothing)
-            float s_own = 0.f;
-#pragma unroll
-            for (int i = 0; i < KPF; ++i) {
-                const f32x4 b = q4[i];
-                s_own += kr[i].x * b.x + kr[i].y * b.y + kr[i].z * b.z + kr[i].w * b.w;
-            }
-            float m = -INFINITY;
-            for (int k = tid; k < S; k += NT) {
-                float s = 0.f;
-                if (k == pos) {
-                    for (int i = 0; i < D4; ++i) {
-                        const f32x4 a = kn4[i], b = q4[i];
-                        s += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
-                    }
-                } else if (k < NT) {
-                    s = s_own;
-                } else {
-                    for (int i = 0; i < D4; ++i) {
-                        const f32x4 a = K4p[(int64_t)k * D4 + i], b = q4[i];
-                        s += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
-                    }
-                }
-                sc[k] = s;
-                m = fmaxf(m, s);
-            }
-            if (li == 1) stamp(110);
-            m = block_max(c, m);
-            if (li == 1) stamp(111);
-            float l = 0.f;
-            for (int k = tid; k < S; k += NT) {
-                const float e = __builtin_amdgcn_exp2f(sc[k] - m);  // q carries log2(e) / sqrt(HD)
-                sc[k] = e;
-                l += e;
-            }
-            l = block_sum(c, l);  // its barriers also publish sc
-            if (li == 1) stamp(112);
-            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            if (rg < R) {
-#pragma unroll
-                for (int t = 0; t < VPF; ++t) {
-                    const int k = rg + t * R;
-                    if (k < pos) acc += sc[k] * vr[t];
-                }
-                for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
-                if (pos % R == rg) acc += sc[pos] * vn4[d4];
-            }
-            if (li == 1) stamp(113);
-            f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
-            if (rg < R) part[rg * D4 + d4] = acc;
-            lds_barrier();
-            if (li == 1) stamp(114);
-            if (tid < D4) {
-                f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 8
-                for (int r = 0; r < R; ++r) o += part[r * D4 + tid];
-                o *= 1.0f / l;
-                gput(g_o + qo + 4 * tid + 0, tag, o.x);
-                gput(g_o + qo + 4 * tid + 1, tag, o.y);
-                gput(g_o + qo + 4 * tid + 2, tag, o.z);
-                gput(g_o + qo + 4 * tid + 3, tag, o.w);
-            }
-            stamp(4 + 10 * li);
-        }
-        // ---- stage C: O-proj + residual (llama3.py:211, 253) --------------------------------
-        {
-            bool valid;
-            const int u = stage_unit(p, D, wg, valid);
-            const int row[1] = {u};
-            f32x4 w[1][NCD];
-            load_rows<1, NCD>(p.wo[li], row, K4q, valid, w);
-            if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
-            stamp(5 + 10 * li);
-            float acc[1];
-            dot_rows<1, NCD>(w, xs, K4q, acc);
-            if (valid && tid % LPR == 0) gput(g_h1 + u, tag, hin[u] + acc[0]);
-            stamp(6 + 10 * li);
-        }
-        // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) -----------------------
-        {
-            bool valid;
-            const int u = stage_unit(p, FD, wg, valid);  // hidden unit: fused rows 32(u/16) + u%16, +16
-            const int row[2] = {32 * (u / 16) + u % 16, 32 * (u / 16) + u % 16 + 16};
-            f32x4 w[2][NCD];
-            load_rows<2, NCD>(p.wgu[li], row, K4d, valid, w);
-            if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
-            stamp(7 + 10 * li);
-            const float rs = inv_rms(c, h1s, D);
-            float acc[2];
-            dot_rows<2, NCD>(w, h1s, K4d, acc);
-            if (valid && tid % LPR == 0) {
-                const float g = acc[0] * rs, up = acc[1] * rs;
-                gput(g_hid + u, tag, g * __builtin_amdgcn_rcpf(1.0f + __expf(-g)) * up);
-            }
-            stamp(8 + 10 * li);
-        }
-        // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
-        {
-            bool valid;
-            const int u = stage_unit(p, D, wg, valid);
-            const int row[1] = {u};
-            f32x4 w[1][NCF];
-            load_rows<1, NCF>(p.wd[li], row, K4f, valid, w);
-            if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
-            stamp(9 + 10 * li);
-            float acc[1];
-            dot_rows<1, NCF>(w, xs, K4f, acc);
-            if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);
-            stamp(10 + 10 * li);
-        }
-    }
-    if (layer_wg) {
-        if (wg != 0) goto done;
-        if (p.write_id) goto final;  // the final argmax (the last step of a graph)
-        // the next launch reduces this step's partials itself; only the position moves on here
-        // (every layer workgroup read it at its start: none could have finished layer 0 else)
-        if (tid == 0) p.st->pos = pos + 1;
-        goto done;
-    }
-
-    // ---- final RMSNorm + lm_head (llama3.py:304-307) + this workgroup's argmax (:320) ---------
-    {
-        u64* g_last = p.gran + slab * (p.n_layers - 1) + qkvn + qdim + D + FD;
+        u64* g_last = p.gran + slab * (p.n_layers - 1) + h2_off;
         if (tid == 0) {  // a long wait: one lane polls the last granule, sleeping
             for (unsigned spin = 0; (unsigned)(gget(g_last + D - 1) >> 32) != tag; ++spin) {
                 if (spin > (1u << 20)) break;
@@ -552,8 +305,296 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         stamp(101);
         goto done;
     }
-final:
-    // ---- workgroup 0: the step's greedy id from the lm partials; generate history, position ----
+
+    // from_parts: the previous step (the launch before this one in the same graph) left its
+    // lm_head partials and no id; every layer workgroup reduces them itself (plain loads: written
+    // by the previous launch) — its final argmax hand-off and reduction come off that step's tail.
+    // This launch's own partials overwrite them only after every layer workgroup has started
+    // (the lm stage waits for the whole layer chain, which needs every layer workgroup).
+    if (p.from_parts) {  // (layer workgroups only from here on)
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < nlm; i += NT) {
+            const u64 v = lm_g[2 * i], x = lm_g[2 * i + 1];
+            const float bv = __uint_as_float((unsigned)v);
+            const int ix = (int)(unsigned)x;
+            const bool take = argmax_better(bv, ix, best, bi);
+            best = take ? bv : best;
+            bi = take ? ix : bi;
+        }
+        group_argmax<64>(best, bi, tid & 63);
+        __shared__ float pb[4];
+        __shared__ int pi[4];
+        if ((tid & 63) == 0) { pb[tid >> 6] = best; pi[tid >> 6] = bi; }
+        lds_barrier();
+        best = pb[0];
+        bi = pi[0];
+        for (int w2 = 1; w2 < 4; ++w2) {
+            const bool take = argmax_better(pb[w2], pi[w2], best, bi);
+            best = take ? pb[w2] : best;
+            bi = take ? pi[w2] : bi;
+        }
+        id = bi;
+        if (wg == 0 && tid == 0) {  // the previous step's id: its generate history entry
+            const int q = pos - 1 - hist_base;
+            if (hist && q >= 0 && q < hist_cap) hist[q] = id;
+        }
+    }
+
+    for (int li = 0; li < p.n_layers; ++li) {
+        u64* g_qkv = p.gran + slab * li;
+        u64* g_op = g_qkv + qkvn;
+        u64* g_hid = g_op + (int64_t)H * D;
+        u64* g_h2 = g_hid + FD;
+        const float* wqkv = p.wqkv[li];
+        float* ck = p.cache_k[li];
+        float* cv = p.cache_v[li];
+        // the attention workgroups' K / V rows of this layer (keys before pos: written by earlier
+        // launches) go out first, at the layer's start: they come from the MALL / HBM (~1 us),
+        // which the QKV stage and its hand-off now cover (issued after it, stage B waited on them)
+        const int kvh = wg / (H / KVH);
+        const int D4 = HD / 4, R = NT / D4;  // PV: R key groups x D4 float4 columns
+        const int rg = tid / D4, d4 = tid - rg * D4;
+        const f32x4* K4p = reinterpret_cast<const f32x4*>(ck + (int64_t)kvh * p.Smax * HD);
+        const f32x4* V4p = reinterpret_cast<const f32x4*>(cv + (int64_t)kvh * p.Smax * HD);
+        constexpr int VPF = (NT + NT / KPF - 1) / (NT / KPF);  // V rows per lane: the first NT keys
+        // unpredicated loads from clamped rows (see load_rows), zeroed where used; row pos - 1 is
+        // the last one an earlier launch wrote (pos >= 1 in a decode step)
+        const int kmax = pos > 0 ? pos - 1 : 0;
+        const gf4p Kg = gf4(K4p), Vg = gf4(V4p);
+        // (wo4: this head's O-proj columns Wo[:, h HD:(h + 1) HD], lane (rg, d4): rows rg + R j,
+        // float4 column d4 — loaded in stage B once the K rows are dead)
+        constexpr int WOR = (64 * NCD + NT / KPF - 1) / (NT / KPF);  // rows per lane (D <= 64 NCD)
+        f32x4 kr[KPF], vr[VPF], wo4[WOR];
+        if (wg < H) {
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
+#pragma unroll
+            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + min(d4, D4 - 1)];
+        }
+        // ---- stage A: RMSNorm + QKV + RoPE + KV append (llama3.py:248, 166-185) -------------
+        {
+            bool valid;
+            const int u = stage_unit(p, qkvn / 2, wg, valid);  // RoPE pair (rows 2u, 2u + 1)
+            const int row[2] = {2 * u, 2 * u + 1};
+            f32x4 w[2][NCD];
+            load_rows<2, NCD>(wqkv, row, K4d, valid, w);
+            const int col = 2 * u;
+            const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
+            const int cc = col - (sec == 0 ? 0 : sec == 1 ? qdim : qdim + kvdim);
+            const int head = cc / HD, d = cc - head * HD;
+            float2 cs = {1.f, 0.f};
+            if (sec < 2) {
+                const int t = pos * (HD >> 1) + (d >> 1);
+                cs = float2{p.rope_cos[t], p.rope_sin[t]};
+            }
+            float* cache = sec == 1 ? ck : cv;
+            const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
+            float2 old = {0.f, 0.f};
+            if (p.kv_bak && sec > 0 && valid) old = *reinterpret_cast<const float2*>(cache + coff);
+            // the layer input: the token's embedding row (llama3.py:287), else the previous
+            // layer's output granules
+            if (li == 0) {
+                for (int i = tid; i < D; i += NT) hin[i] = p.emb[(int64_t)id * D + i];
+                lds_barrier();
+            } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
+                goto done;
+            }
+            stamp(1 + 10 * li);
+            const float rs = inv_rms(c, hin, D);
+            float acc[2];
+            dot_rows<2, NCD>(w, hin, K4d, acc);
+            if (valid && tid % LPR == 0) {
+                const float v0 = acc[0] * rs, v1 = acc[1] * rs;
+                const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
+                const float s = sec == 0 ? p.q_scale : 1.0f;
+                gput(g_qkv + col, tag, r0 * s);
+                gput(g_qkv + col + 1, tag, r1 * s);
+                if (sec > 0) {
+                    if (p.kv_bak)  // [pos % KV_BAK_SLOTS][k, v][1][KVH][HD]: the slot it overwrites
+                        *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer +
+                                                   (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d) = old;
+                    *reinterpret_cast<float2*>(cache + coff) = float2{r0, r1};
+                }
+            }
+            stamp(2 + 10 * li);
+        }
+        // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
+        if (wg < H) {
+            const int h = wg;
+            float* qs = xs;                              // q | k_new | v_new of this head
+            const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
+            if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
+                goto done;
+            stamp(3 + 10 * li);
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) kr[i] = (i < D4 && tid < pos) ? kr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < VPF; ++t) vr[t] = (rg < R && rg + t * R < pos) ? vr[t] : f32x4{0.f, 0.f, 0.f, 0.f};
+            const f32x4* q4 = reinterpret_cast<const f32x4*>(qs);
+            const f32x4* kn4 = reinterpret_cast<const f32x4*>(qs + HD);
+            const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
+            const int S = pos + 1;
+            // key tid from the prefetched row (rows past HD are zero: the q4 reads past HD land
+            // in the k / v part of qs and add nothing); the new key (tid == pos) from k_new, in
+            // the same unrolled pass — a lane of its own looping over LDS held its whole wave
+            // (and the block_max barrier) back ~0.7 us
+            if (tid == pos) {
+#pragma unroll
+                for (int i = 0; i < KPF; ++i) kr[i] = i < D4 ? kn4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            float s_own = 0.f;
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) {
+                const f32x4 b = q4[i];
+                s_own += kr[i].x * b.x + kr[i].y * b.y + kr[i].z * b.z + kr[i].w * b.w;
+            }
+            {  // this head's O-proj columns (the K rows are dead now), landing during softmax + P.V
+                const gf4p Wg = gf4(reinterpret_cast<const f32x4*>(p.wo[li]));
+#pragma unroll
+                for (int j = 0; j < WOR; ++j) wo4[j] = Wg[(int64_t)min(rg + R * j, D - 1) * K4q + wg * D4 + min(d4, D4 - 1)];
+            }
+            float m = -INFINITY;
+            if (tid < S) {
+                sc[tid] = s_own;
+                m = s_own;
+            }
+            for (int k = tid + NT; k < S; k += NT) {
+                float s = 0.f;
+                // keys past the first NT (contexts longer than a workgroup; off the stories path):
+                // a plain loop — an unrolled row here held registers over the whole stage
+                for (int i = 0; i < D4; ++i) {
+                    const f32x4 a = k == pos ? kn4[i] : K4p[(int64_t)k * D4 + i], b = q4[i];
+                    s += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+                }
+                sc[k] = s;
+                m = fmaxf(m, s);
+            }
+            if (li == 1) stamp(110);
+            m = block_max(c, m);
+            if (li == 1) stamp(111);
+            float l = 0.f;
+            for (int k = tid; k < S; k += NT) {
+                const float e = __builtin_amdgcn_exp2f(sc[k] - m);  // q carries log2(e) / sqrt(HD)
+                sc[k] = e;
+                l += e;
+            }
+            l = block_sum(c, l);  // its barriers also publish sc
+            if (li == 1) stamp(112);
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            if (rg < R) {
+#pragma unroll
+                for (int t = 0; t < VPF; ++t) {
+                    const int k = rg + t * R;
+                    if (k < pos) acc += sc[k] * vr[t];
+                }
+                for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
+                if (pos % R == rg) acc += sc[pos] * vn4[d4];
+            }
+            if (li == 1) stamp(113);
+            f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
+            if (rg < R) part[rg * D4 + d4] = acc;
+            lds_barrier();
+            if (li == 1) stamp(114);
+            float* ov = sc + p.Smax + 4 + NT * 4;  // [HD] this head's output row
+            float* opart = ov + 64;                 // [D][D4 + 1] O-proj partial sums
+            if (tid < D4) {
+                // the first NT / KPF key groups' partials read in one go (R >= that: D4 <= KPF),
+                // then added in order (a loop of read-wait-add was ~0.9 us of LDS round trips)
+                constexpr int RC = NT / KPF;
+                f32x4 pr[RC];
+#pragma unroll
+                for (int r = 0; r < RC; ++r) pr[r] = part[r * D4 + tid];
+                f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int r = 0; r < RC; ++r) o += pr[r];
+                for (int r = RC; r < R; ++r) o += part[r * D4 + tid];
+                o *= 1.0f / l;
+                reinterpret_cast<f32x4*>(ov)[tid] = o;
+            }
+            lds_barrier();
+            // O-proj folded in (llama3.py:211): this head's partial rows Wo[:, h HD:(h + 1) HD] . o_h
+            // for all D outputs; the gate|up stage adds the H partials to the residual — no O-proj
+            // stage and no hand-off of its own
+            if (rg < R) {
+                const f32x4 o4 = reinterpret_cast<const f32x4*>(ov)[d4];
+#pragma unroll
+                for (int j = 0; j < WOR; ++j) {
+                    const int r = rg + R * j;
+                    const f32x4 w = wo4[j];
+                    if (r < D) opart[r * (D4 + 1) + d4] = w.x * o4.x + w.y * o4.y + w.z * o4.z + w.w * o4.w;
+                }
+            }
+            lds_barrier();
+            if (li == 1) stamp(115);
+            for (int r = tid; r < D; r += NT) {
+                float x[KPF];
+#pragma unroll
+                for (int i = 0; i < KPF; ++i) x[i] = opart[r * (D4 + 1) + min(i, D4 - 1)];
+                float sum = 0.f;
+#pragma unroll
+                for (int i = 0; i < KPF; ++i) sum += i < D4 ? x[i] : 0.f;
+                gput(g_op + (int64_t)h * D + r, tag, sum);
+            }
+            stamp(4 + 10 * li);
+        }
+        // ---- stage D: residual + the heads' O-proj partials (llama3.py:253), RMSNorm + gate|up
+        //      + SwiGLU (llama3.py:256, 97-101) ---------------------------------------------------
+        {
+            bool valid;
+            const int u = stage_unit(p, FD, wg, valid);  // hidden unit: fused rows 32(u/16) + u%16, +16
+            const int row[2] = {32 * (u / 16) + u % 16, 32 * (u / 16) + u % 16 + 16};
+            f32x4 w[2][NCD];
+            load_rows<2, NCD>(p.wgu[li], row, K4d, valid, w);
+            if (!sweep<8>(c, g_op, H * D, xs, [](int i) { return i; })) goto done;  // H D <= 8 NT
+            stamp(7 + 10 * li);
+            // h1 = h + sum over heads in head order (every workgroup the same sum: the down stage's
+            // residual); the partials read 8 at a time
+            for (int i = tid; i < D; i += NT) {
+                float s = hin[i];
+                for (int h0 = 0; h0 < H; h0 += 8) {
+                    float x[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) x[k] = xs[min(h0 + k, H - 1) * D + i];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s += h0 + k < H ? x[k] : 0.f;
+                }
+                h1s[i] = s;
+            }
+            lds_barrier();
+            const float rs = inv_rms(c, h1s, D);
+            float acc[2];
+            dot_rows<2, NCD>(w, h1s, K4d, acc);
+            if (valid && tid % LPR == 0) {
+                const float g = acc[0] * rs, up = acc[1] * rs;
+                gput(g_hid + u, tag, g * __builtin_amdgcn_rcpf(1.0f + __expf(-g)) * up);
+            }
+            stamp(8 + 10 * li);
+        }
+        // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
+        {
+            bool valid;
+            const int u = stage_unit(p, D, wg, valid);
+            const int row[1] = {u};
+            f32x4 w[1][NCF];
+            load_rows<1, NCF>(p.wd[li], row, K4f, valid, w);
+            if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
+            stamp(9 + 10 * li);
+            float acc[1];
+            dot_rows<1, NCF>(w, xs, K4f, acc);
+            if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);
+            stamp(10 + 10 * li);
+        }
+    }
+    if (wg != 0) goto done;
+    if (!p.write_id) {
+        // the next launch reduces this step's partials itself; only the position moves on here
+        // (every layer workgroup read it at its start: none could have finished layer 0 else)
+        if (tid == 0) p.st->pos = pos + 1;
+        goto done;
+    }
+
+    // ---- workgroup 0, last step of a graph: the step's greedy id from the lm partials; generate history, position ----
     {
         float* pv = xs;  // [2 nlm]
         if (sweep_n(c, lm_g, 2 * nlm, pv, [](int i) { return i; })) {
@@ -597,7 +638,7 @@ bool decode_persist_ok(const DecodePersistArgs& a) {
            a.H % a.KVH == 0 && a.H * a.HD == a.D && ncd_of(a.D) && ncf_of(a.FD) && qkvn % 2 == 0 &&
            (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD + a.GL - 1) / a.GL <= persist::UPP &&
            (a.D + a.GL - 1) / a.GL <= persist::UPP && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
-           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256;
+           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256 && a.H * a.D <= 8 * persist::NT;
 }
 
 // Grid of one decode step: one workgroup per CU (256 on MI355X; every one resident: 1 per CU by
@@ -610,7 +651,9 @@ hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s) {
         return hipErrorNotSupported;
     const int grid = cus < 256 ? cus : 256;
     if (grid <= a.GL || 2 * (grid - a.GL) > a.Xp) return hipErrorNotSupported;
-    const size_t lds = ((size_t)2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
+    // hin, h1s, xs, scores, P.V partials, o_h, O-proj partials [D][HD / 4 + 1]
+    const size_t lds = ((size_t)2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64 + (size_t)a.D * (a.HD / 4 + 1)) * 4;
+    if (a.Xp < a.H * a.D || lds > 64 * 1024) return hipErrorNotSupported;  // (default dynamic LDS cap)
     const int ncd = ncd_of(a.D), ncf = ncf_of(a.FD);
 #define L3_PERSIST(NCD, NCF, KPF, LMPF)                                                            \
     if (ncd == NCD && ncf == NCF) {                                                                \

@@ -265,6 +265,10 @@ struct DecodePersistArgs {
     unsigned* err;                 // host-mapped: set to 1 when a workgroup gave up on a hand-off
     unsigned long long* stamps;    // diagnostic (null): [workgroup][128] s_memrealtime at stage points
 };
+// granules per layer of the persistent step: [qkv | O-proj partials H x D | hid | h2]
+__host__ __device__ inline int64_t decode_persist_slab(int H, int KVH, int HD, int D, int FD) {
+    return (int64_t)(H + 2 * KVH) * HD + (int64_t)H * D + FD + D;
+}
 bool decode_persist_ok(const DecodePersistArgs& a);
 hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s);
 

@@ -976,12 +976,13 @@ static int persist_setup(l3_ctx* c) {
     int xp = c->qkvn > a.FD ? c->qkvn : a.FD;
     if (xp < 3 * a.HD) xp = 3 * a.HD;
     if (xp < 512) xp = 512;  // the final argmax's 2 x 256 partials
+    if (xp < a.H * a.D) xp = a.H * a.D;  // the O-proj partials of every head
     a.Xp = (xp + 3) & ~3;
     a.eps = c->d.norm_eps;
     a.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     a.emb = c->emb; a.lm_head = c->lm_head; a.rope_cos = c->rope_cos; a.rope_sin = c->rope_sin;
     a.bak_layer = (int64_t)KV_BAK_SLOTS * 2 * 8 * c->d.n_kv_heads * c->HD;
-    const int64_t slab = (int64_t)c->qkvn + c->qdim + a.D + a.FD + a.D;
+    const int64_t slab = decode_persist_slab(a.H, a.KVH, a.HD, a.D, a.FD);
     const size_t ptr_bytes = (size_t)6 * nl * sizeof(void*);
     const size_t gran_off = (ptr_bytes + 16 + 255) & ~(size_t)255;
     const size_t gran_bytes = (size_t)(slab * nl + 2 * 256) * 8;

@@ -29,7 +29,7 @@ if "--read" not in sys.argv:
 st = np.fromfile(path, dtype=np.uint64).reshape(256, 128).astype(np.int64)
 t0 = st[:, 0][st[:, 0] > 0].min()
 us = lambda x: (x - t0) / 100.0  # noqa: E731
-names = ["qkv", "attn", "oproj", "gateup", "down"]
+names = ["qkv", "attn+o", "oproj", "gateup", "down"]  # (the O-proj rides in attention)
 lay = st[:64]
 
 
@@ -51,8 +51,8 @@ for k, nm in ((0, "start"), (100, "lm input"), (103, "lm rms"), (104, "lm rows d
     a = span(st[:64], k)
     b = span(st[64:], k)
     print(f"  {nm:12s} layer wgs {a[0]}..{a[1]}   lm wgs {b[0]}..{b[1]}")
-print("attention workgroups, layer 1: in / scores / max / sum / PV / part stored / out")
+print("attention workgroups, layer 1: in / scores / max / sum / PV / part stored / O-proj partials / out")
 for h in range(6):
-    print("  head", h, " ".join(f"{us(st[h, k]):7.2f}" for k in (13, 110, 111, 112, 113, 114, 14)))
+    print("  head", h, " ".join(f"{us(st[h, k]):7.2f}" for k in (13, 110, 111, 112, 113, 114, 115, 14)))
 for k, nm in ((105, "wg0 partials in"), (102, "greedy id")):
     print(f"  {nm}: {us(st[0, k]):.2f}")
