@@ -49,6 +49,25 @@ __device__ __forceinline__ void gput(u64* g, unsigned tag, float v) {
 __device__ __forceinline__ u64 gget(u64* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// XCD-local hand-offs (DecodePersistArgs::xcd: every producer and consumer on one XCD, sharing its
+// L2): the store lands in the L2 (the CU's L1 is write-through), the load misses the L1 (sc0) and
+// reads the L2 — no trip through the MALL as the agent-scope (sc1) pair takes.  The load is a
+// buffer load so that the compiler still counts it (vmcnt) like any other.
+__device__ __forceinline__ void gput_xcd(u64* g, unsigned tag, float v) {
+    __hip_atomic_store(g, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ u64 gget_xcd(__amdgpu_buffer_rsrc_t r, int i) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8, 0, 1);  // aux 1: sc0
+    return (u64)(unsigned)v[0] | ((u64)(unsigned)v[1] << 32);
+}
+template <bool LOCAL>
+__device__ __forceinline__ void gput_s(u64* g, unsigned tag, float v) {
+    if (LOCAL) gput_xcd(g, tag, v);
+    else gput(g, tag, v);
+}
+__device__ __forceinline__ unsigned xcc_id() {  // HW_REG_XCC_ID (hwreg 20), bits [3:0]
+    return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((16 - 1) << 11)) & 0xf;
+}
 
 // Workgroup barrier for LDS traffic only: __syncthreads() is also a workgroup-scope release of
 // global memory, i.e. an s_waitcnt vmcnt(0) that waits for this wave's write-through granule /
@@ -77,16 +96,20 @@ __device__ __forceinline__ void give_up(const Ctx& c) {
 // granules g[idx(i)] for i < n into dst[i] (LDS), every thread its i = tid + NT*k, all of a
 // thread's loads in flight per pass; re-read until every tag is the launch's.  Ends with a
 // workgroup barrier; false if this workgroup gave up (caller returns).
-template <int PER, typename Idx>
+template <int PER, bool LOCAL, typename Idx>
 __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
     const int tid = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 0x7fffffff, 0x00020000);
     bool ok = false;
     for (unsigned spin = 0;; ++spin) {
         ok = true;
         u64 x[PER];
         // unpredicated (a clamped index past n: a predicated load is a branch that waits)
 #pragma unroll
-        for (int k = 0; k < PER; ++k) x[k] = gget(g + idx(min(tid + NT * k, n - 1)));
+        for (int k = 0; k < PER; ++k) {
+            const int i = idx(min(tid + NT * k, n - 1));
+            x[k] = LOCAL ? gget_xcd(r, i) : gget(g + i);
+        }
 #pragma unroll
         for (int k = 0; k < PER; ++k) ok &= (unsigned)(x[k] >> 32) == c.tag;
         if (ok) {
@@ -108,11 +131,11 @@ __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, I
     return !*c.bad;
 }
 
-template <typename Idx>
+template <bool LOCAL, typename Idx>
 __device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
-    if (n <= NT) return sweep<1>(c, g, n, dst, idx, sleep);
-    if (n <= 2 * NT) return sweep<2>(c, g, n, dst, idx, sleep);
-    return sweep<4>(c, g, n, dst, idx, sleep);  // n <= 1024 (eligibility)
+    if (n <= NT) return sweep<1, LOCAL>(c, g, n, dst, idx, sleep);
+    if (n <= 2 * NT) return sweep<2, LOCAL>(c, g, n, dst, idx, sleep);
+    return sweep<4, LOCAL>(c, g, n, dst, idx, sleep);  // n <= 1024 (eligibility)
 }
 
 // block sum of one value per thread (every thread gets it)
@@ -202,11 +225,13 @@ __device__ __forceinline__ int stage_unit(const DecodePersistArgs& p, int n, int
 
 }  // namespace persist
 
-// One launch = one decode step.  Granule slab per layer: [qkv | O-proj partials H x D | hid | h2]
+// One launch = one decode step.  Granule slab per layer: [qkv | o | h1 | hid | h2]
 // (decode_persist_slab), then the lm_head partials [2 * gridDim.x].
 // NCD / NCF: float4 per lane of a W row with K = D / K = FD (>= ceil(K / 64)); KPF >= HD / 4; LMPF:
-// lm_head passes of 16 rows each workgroup holds in registers
-template <int NCD, int NCF, int KPF, int LMPF>
+// lm_head passes of 16 rows each workgroup holds in registers.  XL: the layer stages on the 32
+// workgroups of one XCD (wg % 8 == 0; DecodePersistArgs::xcd) with XCD-local hand-offs, two hidden
+// units per gate|up unit; only the last layer's output and the lm partials cross XCDs
+template <int NCD, int NCF, int KPF, int LMPF, bool XL>
 __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArgs p) {
     using namespace persist;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -216,7 +241,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     const int qdim = H * HD, kvdim = KVH * HD, qkvn = qdim + 2 * kvdim;
     float* hin = sm;              // [D]  layer input (residual of the O-proj)
     float* h1s = hin + p.Dp;      // [D]  FFN input (residual of the down-proj)
-    float* xs = h1s + p.Dp;       // [max(qkvn, FD, H D)] stage input
+    float* xs = h1s + p.Dp;       // [max(qkvn, FD, qdim)] stage input
     float* sc = xs + p.Xp;        // [Smax] attention scores
     const int tid = threadIdx.x, wg = blockIdx.x, G = gridDim.x;
     if (tid == 0) bad_s = 0;
@@ -232,21 +257,29 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     };
     stamp(0);
     const int64_t slab = decode_persist_slab(H, KVH, HD, D, FD);
-    const int64_t h2_off = (int64_t)qkvn + (int64_t)H * D + FD;  // h2 within a slab
+    const int64_t h2_off = (int64_t)qkvn + qdim + D + FD;  // h2 within a slab
     u64* lm_g = p.gran + slab * p.n_layers;
     const int K4d = D / 4, K4f = FD / 4, K4q = qdim / 4;
-    const bool layer_wg = wg < p.GL;
+    // roles: layer workgroup lw (the layer stages; the attention of head lw < H) or lm workgroup lwg
+    const bool layer_wg = XL ? wg % 8 == 0 : wg < p.GL;
+    const int lw = XL ? wg / 8 : wg;
 
     // lm_head rows of this workgroup: [r0, r1); unit = one row, LPR lanes.  Only the workgroups
     // past GL take rows: they load them at launch, while the layers run (rows on the layer
     // workgroups were loaded after their last stage and made the final argmax wait ~1 us)
-    const int nlm = G - p.GL, lwg = wg - p.GL;
+    const int nlm = G - p.GL, lwg = XL ? wg - wg / 8 - 1 : wg - p.GL;
     const int lm_per = (p.VS + nlm - 1) / nlm;
-    const int lm_r0 = lwg < 0 ? p.VS : lwg * lm_per, lm_r1 = min(p.VS, lm_r0 + lm_per);
+    const int lm_r0 = layer_wg ? p.VS : lwg * lm_per, lm_r1 = min(p.VS, lm_r0 + lm_per);
     const int lm_passes = lm_r1 > lm_r0 ? (lm_r1 - lm_r0 + UPP - 1) / UPP : 0;
     // the generate-history fields workgroup 0 writes at the end, fetched now (off the final path)
     const int hist_base = p.st->hist_base, hist_cap = p.st->hist_cap;
     int32_t* const hist = p.st->hist;
+    // XL: a layer workgroup off the expected XCD would never see its peers' XCD-local stores —
+    // give up at once (the host checked the placement once, l3::decode_persist_xcd_probe)
+    if (XL && layer_wg && xcc_id() != p.xcc) {
+        if (tid == 0) give_up(c);
+        goto done;
+    }
     if (!layer_wg) {
         // ---- final RMSNorm + lm_head (llama3.py:304-307) + this workgroup's argmax (:320) ---------
         f32x4 lw[LMPF][1][NCD];  // live on this path only (not across the layer loop)
@@ -263,7 +296,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 __builtin_amdgcn_s_sleep(16);
             }
         }
-        if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, 8)) goto done;
+        if (!sweep_n<false>(c, g_last, D, xs, [](int i) { return i; }, 8)) goto done;
         stamp(100);
         const float rs = inv_rms(c, xs, D);
         stamp(103);
@@ -335,7 +368,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             bi = take ? pi[w2] : bi;
         }
         id = bi;
-        if (wg == 0 && tid == 0) {  // the previous step's id: its generate history entry
+        if (lw == 0 && tid == 0) {  // the previous step's id: its generate history entry
             const int q = pos - 1 - hist_base;
             if (hist && q >= 0 && q < hist_cap) hist[q] = id;
         }
@@ -343,8 +376,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
 
     for (int li = 0; li < p.n_layers; ++li) {
         u64* g_qkv = p.gran + slab * li;
-        u64* g_op = g_qkv + qkvn;
-        u64* g_hid = g_op + (int64_t)H * D;
+        u64* g_o = g_qkv + qkvn;
+        u64* g_h1 = g_o + qdim;
+        u64* g_hid = g_h1 + D;
         u64* g_h2 = g_hid + FD;
         const float* wqkv = p.wqkv[li];
         float* ck = p.cache_k[li];
@@ -352,7 +386,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         // the attention workgroups' K / V rows of this layer (keys before pos: written by earlier
         // launches) go out first, at the layer's start: they come from the MALL / HBM (~1 us),
         // which the QKV stage and its hand-off now cover (issued after it, stage B waited on them)
-        const int kvh = wg / (H / KVH);
+        const int kvh = lw / (H / KVH);
         const int D4 = HD / 4, R = NT / D4;  // PV: R key groups x D4 float4 columns
         const int rg = tid / D4, d4 = tid - rg * D4;
         const f32x4* K4p = reinterpret_cast<const f32x4*>(ck + (int64_t)kvh * p.Smax * HD);
@@ -362,11 +396,8 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         // the last one an earlier launch wrote (pos >= 1 in a decode step)
         const int kmax = pos > 0 ? pos - 1 : 0;
         const gf4p Kg = gf4(K4p), Vg = gf4(V4p);
-        // (wo4: this head's O-proj columns Wo[:, h HD:(h + 1) HD], lane (rg, d4): rows rg + R j,
-        // float4 column d4 — loaded in stage B once the K rows are dead)
-        constexpr int WOR = (64 * NCD + NT / KPF - 1) / (NT / KPF);  // rows per lane (D <= 64 NCD)
-        f32x4 kr[KPF], vr[VPF], wo4[WOR];
-        if (wg < H) {
+        f32x4 kr[KPF], vr[VPF];
+        if (lw < H) {
 #pragma unroll
             for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
 #pragma unroll
@@ -375,7 +406,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         // ---- stage A: RMSNorm + QKV + RoPE + KV append (llama3.py:248, 166-185) -------------
         {
             bool valid;
-            const int u = stage_unit(p, qkvn / 2, wg, valid);  // RoPE pair (rows 2u, 2u + 1)
+            const int u = stage_unit(p, qkvn / 2, lw, valid);  // RoPE pair (rows 2u, 2u + 1)
             const int row[2] = {2 * u, 2 * u + 1};
             f32x4 w[2][NCD];
             load_rows<2, NCD>(wqkv, row, K4d, valid, w);
@@ -397,7 +428,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             if (li == 0) {
                 for (int i = tid; i < D; i += NT) hin[i] = p.emb[(int64_t)id * D + i];
                 lds_barrier();
-            } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
+            } else if (!sweep_n<XL>(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
                 goto done;
             }
             stamp(1 + 10 * li);
@@ -408,8 +439,8 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 const float v0 = acc[0] * rs, v1 = acc[1] * rs;
                 const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
                 const float s = sec == 0 ? p.q_scale : 1.0f;
-                gput(g_qkv + col, tag, r0 * s);
-                gput(g_qkv + col + 1, tag, r1 * s);
+                gput_s<XL>(g_qkv + col, tag, r0 * s);
+                gput_s<XL>(g_qkv + col + 1, tag, r1 * s);
                 if (sec > 0) {
                     if (p.kv_bak)  // [pos % KV_BAK_SLOTS][k, v][1][KVH][HD]: the slot it overwrites
                         *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer +
@@ -420,11 +451,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             stamp(2 + 10 * li);
         }
         // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
-        if (wg < H) {
-            const int h = wg;
+        if (lw < H) {
+            const int h = lw;
             float* qs = xs;                              // q | k_new | v_new of this head
             const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
-            if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
+            if (!sweep_n<XL>(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
                 goto done;
             stamp(3 + 10 * li);
 #pragma unroll
@@ -448,11 +479,6 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             for (int i = 0; i < KPF; ++i) {
                 const f32x4 b = q4[i];
                 s_own += kr[i].x * b.x + kr[i].y * b.y + kr[i].z * b.z + kr[i].w * b.w;
-            }
-            {  // this head's O-proj columns (the K rows are dead now), landing during softmax + P.V
-                const gf4p Wg = gf4(reinterpret_cast<const f32x4*>(p.wo[li]));
-#pragma unroll
-                for (int j = 0; j < WOR; ++j) wo4[j] = Wg[(int64_t)min(rg + R * j, D - 1) * K4q + wg * D4 + min(d4, D4 - 1)];
             }
             float m = -INFINITY;
             if (tid < S) {
@@ -496,8 +522,6 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             if (rg < R) part[rg * D4 + d4] = acc;
             lds_barrier();
             if (li == 1) stamp(114);
-            float* ov = sc + p.Smax + 4 + NT * 4;  // [HD] this head's output row
-            float* opart = ov + 64;                 // [D][D4 + 1] O-proj partial sums
             if (tid < D4) {
                 // the first NT / KPF key groups' partials read in one go (R >= that: D4 <= KPF),
                 // then added in order (a loop of read-wait-add was ~0.9 us of LDS round trips)
@@ -510,83 +534,75 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 for (int r = 0; r < RC; ++r) o += pr[r];
                 for (int r = RC; r < R; ++r) o += part[r * D4 + tid];
                 o *= 1.0f / l;
-                reinterpret_cast<f32x4*>(ov)[tid] = o;
-            }
-            lds_barrier();
-            // O-proj folded in (llama3.py:211): this head's partial rows Wo[:, h HD:(h + 1) HD] . o_h
-            // for all D outputs; the gate|up stage adds the H partials to the residual — no O-proj
-            // stage and no hand-off of its own
-            if (rg < R) {
-                const f32x4 o4 = reinterpret_cast<const f32x4*>(ov)[d4];
-#pragma unroll
-                for (int j = 0; j < WOR; ++j) {
-                    const int r = rg + R * j;
-                    const f32x4 w = wo4[j];
-                    if (r < D) opart[r * (D4 + 1) + d4] = w.x * o4.x + w.y * o4.y + w.z * o4.z + w.w * o4.w;
-                }
-            }
-            lds_barrier();
-            if (li == 1) stamp(115);
-            for (int r = tid; r < D; r += NT) {
-                float x[KPF];
-#pragma unroll
-                for (int i = 0; i < KPF; ++i) x[i] = opart[r * (D4 + 1) + min(i, D4 - 1)];
-                float sum = 0.f;
-#pragma unroll
-                for (int i = 0; i < KPF; ++i) sum += i < D4 ? x[i] : 0.f;
-                gput(g_op + (int64_t)h * D + r, tag, sum);
+                gput_s<XL>(g_o + qo + 4 * tid + 0, tag, o.x);
+                gput_s<XL>(g_o + qo + 4 * tid + 1, tag, o.y);
+                gput_s<XL>(g_o + qo + 4 * tid + 2, tag, o.z);
+                gput_s<XL>(g_o + qo + 4 * tid + 3, tag, o.w);
             }
             stamp(4 + 10 * li);
         }
-        // ---- stage D: residual + the heads' O-proj partials (llama3.py:253), RMSNorm + gate|up
-        //      + SwiGLU (llama3.py:256, 97-101) ---------------------------------------------------
+        // ---- stage C: O-proj + residual (llama3.py:211, 253) --------------------------------
         {
             bool valid;
-            const int u = stage_unit(p, FD, wg, valid);  // hidden unit: fused rows 32(u/16) + u%16, +16
-            const int row[2] = {32 * (u / 16) + u % 16, 32 * (u / 16) + u % 16 + 16};
-            f32x4 w[2][NCD];
-            load_rows<2, NCD>(p.wgu[li], row, K4d, valid, w);
-            if (!sweep<8>(c, g_op, H * D, xs, [](int i) { return i; })) goto done;  // H D <= 8 NT
-            stamp(7 + 10 * li);
-            // h1 = h + sum over heads in head order (every workgroup the same sum: the down stage's
-            // residual); the partials read 8 at a time
-            for (int i = tid; i < D; i += NT) {
-                float s = hin[i];
-                for (int h0 = 0; h0 < H; h0 += 8) {
-                    float x[8];
+            const int u = stage_unit(p, D, lw, valid);
+            const int row[1] = {u};
+            f32x4 w[1][NCD];
+            load_rows<1, NCD>(p.wo[li], row, K4q, valid, w);
+            if (!sweep_n<XL>(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
+            stamp(5 + 10 * li);
+            float acc[1];
+            dot_rows<1, NCD>(w, xs, K4q, acc);
+            if (valid && tid % LPR == 0) gput_s<XL>(g_h1 + u, tag, hin[u] + acc[0]);
+            stamp(6 + 10 * li);
+        }
+        // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) -----------------------
+        {
+            bool valid;
+            // unit u: hidden units GU u .. GU u + GU - 1; hidden unit v: fused rows 32(v/16) + v%16, +16
+            constexpr int GU = XL ? 2 : 1;
+            const int u = stage_unit(p, FD / GU, lw, valid);
+            int row[2 * GU];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) x[k] = xs[min(h0 + k, H - 1) * D + i];
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s += h0 + k < H ? x[k] : 0.f;
-                }
-                h1s[i] = s;
+            for (int g = 0; g < GU; ++g) {
+                const int v = GU * u + g;
+                row[2 * g] = 32 * (v / 16) + v % 16;
+                row[2 * g + 1] = row[2 * g] + 16;
             }
-            lds_barrier();
+            f32x4 w[2 * GU][NCD];
+            load_rows<2 * GU, NCD>(p.wgu[li], row, K4d, valid, w);
+            if (!sweep_n<XL>(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
+            stamp(7 + 10 * li);
             const float rs = inv_rms(c, h1s, D);
-            float acc[2];
-            dot_rows<2, NCD>(w, h1s, K4d, acc);
+            float acc[2 * GU];
+            dot_rows<2 * GU, NCD>(w, h1s, K4d, acc);
             if (valid && tid % LPR == 0) {
-                const float g = acc[0] * rs, up = acc[1] * rs;
-                gput(g_hid + u, tag, g * __builtin_amdgcn_rcpf(1.0f + __expf(-g)) * up);
+#pragma unroll
+                for (int g = 0; g < GU; ++g) {
+                    const float gt = acc[2 * g] * rs, up = acc[2 * g + 1] * rs;
+                    gput_s<XL>(g_hid + GU * u + g, tag, gt * __builtin_amdgcn_rcpf(1.0f + __expf(-gt)) * up);
+                }
             }
             stamp(8 + 10 * li);
         }
         // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
         {
             bool valid;
-            const int u = stage_unit(p, D, wg, valid);
+            const int u = stage_unit(p, D, lw, valid);
             const int row[1] = {u};
             f32x4 w[1][NCF];
             load_rows<1, NCF>(p.wd[li], row, K4f, valid, w);
-            if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
+            if (!sweep_n<XL>(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
             stamp(9 + 10 * li);
             float acc[1];
             dot_rows<1, NCF>(w, xs, K4f, acc);
-            if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);
+            if (valid && tid % LPR == 0) {  // the last layer's output goes to the lm workgroups
+                if (XL && li + 1 < p.n_layers) gput_xcd(g_h2 + u, tag, h1s[u] + acc[0]);
+                else gput(g_h2 + u, tag, h1s[u] + acc[0]);
+            }
             stamp(10 + 10 * li);
         }
     }
-    if (wg != 0) goto done;
+    if (lw != 0) goto done;  // (wg 0 in both layouts)
     if (!p.write_id) {
         // the next launch reduces this step's partials itself; only the position moves on here
         // (every layer workgroup read it at its start: none could have finished layer 0 else)
@@ -597,7 +613,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     // ---- workgroup 0, last step of a graph: the step's greedy id from the lm partials; generate history, position ----
     {
         float* pv = xs;  // [2 nlm]
-        if (sweep_n(c, lm_g, 2 * nlm, pv, [](int i) { return i; })) {
+        if (sweep_n<false>(c, lm_g, 2 * nlm, pv, [](int i) { return i; })) {
             stamp(105);
             float best = -INFINITY;
             int bi = 0x7fffffff;
@@ -634,11 +650,38 @@ static int ncf_of(int FD) { const int n = (FD + 63) / 64; return n <= 3 ? 3 : n 
 
 bool decode_persist_ok(const DecodePersistArgs& a) {
     const int qkvn = (a.H + 2 * a.KVH) * a.HD;
+    const int gu = a.xcd ? 2 : 1;  // hidden units per gate|up unit
     return a.D % 4 == 0 && a.FD % 4 == 0 && a.HD % 4 == 0 && a.HD >= 4 && a.HD <= 64 && a.H <= a.GL &&
            a.H % a.KVH == 0 && a.H * a.HD == a.D && ncd_of(a.D) && ncf_of(a.FD) && qkvn % 2 == 0 &&
-           (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD + a.GL - 1) / a.GL <= persist::UPP &&
+           (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD / gu + a.GL - 1) / a.GL <= persist::UPP &&
            (a.D + a.GL - 1) / a.GL <= persist::UPP && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
-           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256 && a.H * a.D <= 8 * persist::NT;
+           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256 && (!a.xcd || a.GL == 32);
+}
+
+// Which XCD the workgroups of a 256-workgroup grid run on: the hardware deals workgroups to the
+// 8 XCDs round-robin (SPX mode), so wg % 8 == 0 share one — checked here once, before the
+// one-XCD layout (DecodePersistArgs::xcd) is used.
+__global__ void xcc_probe_kernel(unsigned* out) {
+    if (threadIdx.x == 0) out[blockIdx.x] = persist::xcc_id();
+}
+
+int decode_persist_xcd_probe(unsigned* xcc) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 256)
+        return 0;
+    unsigned* d = nullptr;
+    unsigned h[256];
+    if (hipMalloc(&d, sizeof h) != hipSuccess) return 0;
+    bool ok = true;
+    for (int rep = 0; rep < 3 && ok; ++rep) {
+        hipLaunchKernelGGL(xcc_probe_kernel, dim3(256), dim3(256), 0, 0, d);
+        ok = hipDeviceSynchronize() == hipSuccess && hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
+        for (int i = 0; i < 256 && ok; ++i) ok = (i % 8 == 0) == (h[i] == h[0]);
+    }
+    (void)hipFree(d);
+    if (ok) *xcc = h[0];
+    return ok ? 1 : 0;
 }
 
 // Grid of one decode step: one workgroup per CU (256 on MI355X; every one resident: 1 per CU by
@@ -650,14 +693,17 @@ hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return hipErrorNotSupported;
     const int grid = cus < 256 ? cus : 256;
-    if (grid <= a.GL || 2 * (grid - a.GL) > a.Xp) return hipErrorNotSupported;
-    // hin, h1s, xs, scores, P.V partials, o_h, O-proj partials [D][HD / 4 + 1]
-    const size_t lds = ((size_t)2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64 + (size_t)a.D * (a.HD / 4 + 1)) * 4;
-    if (a.Xp < a.H * a.D || lds > 64 * 1024) return hipErrorNotSupported;  // (default dynamic LDS cap)
+    if (grid <= a.GL || 2 * (grid - a.GL) > a.Xp || (a.xcd && grid != 256)) return hipErrorNotSupported;
+    // hin, h1s, xs, scores, P.V partials
+    const size_t lds = ((size_t)2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
+    if (lds > 64 * 1024) return hipErrorNotSupported;  // (the default dynamic LDS cap)
     const int ncd = ncd_of(a.D), ncf = ncf_of(a.FD);
 #define L3_PERSIST(NCD, NCF, KPF, LMPF)                                                            \
     if (ncd == NCD && ncf == NCF) {                                                                \
-        hipLaunchKernelGGL((decode_persist_kernel<NCD, NCF, KPF, LMPF>), dim3(grid), dim3(256), lds, s, a); \
+        if (a.xcd)                                                                                 \
+            hipLaunchKernelGGL((decode_persist_kernel<NCD, NCF, KPF, LMPF, true>), dim3(grid), dim3(256), lds, s, a); \
+        else                                                                                       \
+            hipLaunchKernelGGL((decode_persist_kernel<NCD, NCF, KPF, LMPF, false>), dim3(grid), dim3(256), lds, s, a); \
         return hipGetLastError();                                                                  \
     }
     L3_PERSIST(1, 3, 16, 8)   // tiny models (tests)

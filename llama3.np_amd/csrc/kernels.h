@@ -11,7 +11,7 @@ namespace l3 {
 //   runtime.hip  L3_BATCH_SPLIT (2), L3_LAST_LAYER_ALL_ROWS (0), L3_DECODE_FUSE_O (1),
 //                L3_LM_AMAX (1), L3_DECODE_FOLD_ARGMAX (1), L3_DECODE_SPECULATE (1), L3_DECODE_GRAPH_STEPS (8),
 //                L3_DECODE_GRAPH (1), L3_COMM_MODE (1), L3_COMM_PRIORITY (1), L3_GROUP_MULTI_PATH (0),
-//                L3_DECODE_PERSIST (0)
+//                L3_DECODE_PERSIST (0; 1 all-XCD layout, 2 one-XCD layout)
 //   gemm.hip     L3_SPLITK (1), L3_SPLITK_CFG (0), L3_SPLITK_BLOCKS (1024), L3_SPLITK_MINKT (8),
 //                L3_GEMV_NT (1), L3_GEMV_LPU (0 = by shape), L3_GEMV_MR (by shape), L3_SKINNY (1),
 //                L3_SKINNY_MIN (9)
@@ -241,7 +241,10 @@ __device__ __forceinline__ int start_of(const Args& p) {
 // every layer, the lm_head and the argmax — with in-launch hand-offs between the stages
 struct DecodePersistArgs {
     int D, H, KVH, HD, FD, VS, n_layers, Smax;
-    int GL;                        // workgroups that run the layer stages (the lm_head uses all 256)
+    int GL;                        // workgroups that run the layer stages (the others: the lm_head)
+    int xcd;                       // 1: the layer stages on one XCD (GL = 32, wg % 8 == 0), XCD-local
+                                   //    hand-offs; 0: GL = 64 workgroups over all XCDs
+    unsigned xcc;                  // xcd: the XCD id the layer workgroups must find (checked)
     int Dp, Xp;                    // LDS floats: per D-vector, per stage-input vector (multiples of 4)
     float eps, q_scale;
     const float* emb;              // [VS, D]
@@ -265,12 +268,13 @@ struct DecodePersistArgs {
     unsigned* err;                 // host-mapped: set to 1 when a workgroup gave up on a hand-off
     unsigned long long* stamps;    // diagnostic (null): [workgroup][128] s_memrealtime at stage points
 };
-// granules per layer of the persistent step: [qkv | O-proj partials H x D | hid | h2]
+// granules per layer of the persistent step: [qkv | o | h1 | hid | h2]
 __host__ __device__ inline int64_t decode_persist_slab(int H, int KVH, int HD, int D, int FD) {
-    return (int64_t)(H + 2 * KVH) * HD + (int64_t)H * D + FD + D;
+    return (int64_t)(H + 2 * KVH) * HD + (int64_t)H * HD + D + FD + D;
 }
 bool decode_persist_ok(const DecodePersistArgs& a);
 hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s);
+int decode_persist_xcd_probe(unsigned* xcc);  // 1: wg % 8 == 0 share one XCD (its id in *xcc)
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);

@@ -211,6 +211,9 @@ struct l3_ctx {
     DecodePersistArgs persist{};
     bool persist_ready = false;
     bool persist_graph = false;      // the captured single-step graph runs the persistent step
+    int persist_xcd_ok = -1;         // wg % 8 == 0 on one XCD (decode_persist_xcd_probe); -1: not probed
+    unsigned persist_xcc = 0;
+    bool persist_xcd = false;        // this capture: the one-XCD layout (L3_DECODE_PERSIST=2)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -952,16 +955,22 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
     return 0;
 }
 
-// Persistent batch-1 decode step (decode_persist.hip): L3_DECODE_PERSIST=1 (A/B) and a shape the
-// kernel takes (decode_persist_ok).  Its buffers are made once, with the stream idle.
+// Persistent batch-1 decode step (decode_persist.hip): L3_DECODE_PERSIST=1 (layer stages on 64
+// workgroups over all XCDs) or 2 (on the 32 workgroups of one XCD, if the placement probe agrees;
+// else 1), and a shape the kernel takes (decode_persist_ok).  Its buffers are made once, with the
+// stream idle.
 static bool persist_wanted(l3_ctx* c, int B) {
-    // read at every capture (captures are rare), so a process can A/B both paths
-    const bool on = env_knob("L3_DECODE_PERSIST", 0) != 0;
-    if (!on || B != 1 || c->layers.empty() || !c->dec_state) return false;
-    if (c->persist_ready) return true;
+    // read at every capture (captures are rare), so a process can A/B the paths
+    const int mode = env_knob("L3_DECODE_PERSIST", 0);
+    if (!mode || B != 1 || c->layers.empty() || !c->dec_state) return false;
+    if (mode == 2 && c->persist_xcd_ok < 0) c->persist_xcd_ok = decode_persist_xcd_probe(&c->persist_xcc);
     DecodePersistArgs a{};
     a.D = c->d.dim; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads; a.HD = c->HD; a.FD = c->d.hidden_dim;
-    a.VS = c->d.vocab_size; a.n_layers = (int)c->layers.size(); a.Smax = c->d.max_seq_len; a.GL = 64;
+    a.VS = c->d.vocab_size; a.n_layers = (int)c->layers.size(); a.Smax = c->d.max_seq_len;
+    a.xcd = mode == 2 && c->persist_xcd_ok == 1;
+    a.GL = a.xcd ? 32 : 64;
+    if (a.xcd && !decode_persist_ok(a)) { a.xcd = 0; a.GL = 64; }
+    c->persist_xcd = a.xcd != 0;
     return decode_persist_ok(a);
 }
 
@@ -976,7 +985,6 @@ static int persist_setup(l3_ctx* c) {
     int xp = c->qkvn > a.FD ? c->qkvn : a.FD;
     if (xp < 3 * a.HD) xp = 3 * a.HD;
     if (xp < 512) xp = 512;  // the final argmax's 2 x 256 partials
-    if (xp < a.H * a.D) xp = a.H * a.D;  // the O-proj partials of every head
     a.Xp = (xp + 3) & ~3;
     a.eps = c->d.norm_eps;
     a.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
@@ -1057,6 +1065,9 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
         a.ids = c->dec_ids;
         a.st = c->dec_state;
         a.kv_bak = c->bak_capture ? c->kv_bak : nullptr;
+        a.xcd = c->persist_xcd ? 1 : 0;
+        a.GL = a.xcd ? 32 : 64;
+        a.xcc = c->persist_xcc;
         a.from_parts = i > 0;            // the previous step in this graph left partials only
         a.write_id = i == steps - 1;     // the last one publishes the id for the host / next graph
         const hipError_t e = launch_decode_persist(a, c->stream);

@@ -15,7 +15,9 @@ from typing import List, Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "csrc", "libllama3hip.so")
+# L3_LIB_PATH: another build of the same library (kernel A/B runs in one box call, tools/ab_lib.sh);
+# the product always loads the in-tree build
+LIB_PATH = os.environ.get("L3_LIB_PATH") or os.path.join(HERE, "csrc", "libllama3hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "llama3hip.h")
 
 # weight kinds / kernel ids (mirror the enums in include/llama3hip.h)
