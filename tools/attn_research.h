@@ -15,6 +15,8 @@ namespace l3 {
 // done, [3 + 2t] after tile t's barrier (t < 4), [10] exit, [11] HW_REG_HW_ID, [12] XCC_ID
 __device__ unsigned long long* g_attn_stamps;
 
+// ABL & 2048 / 4096: hand-ordered score / P.V phases of the unmasked body (sched_group_barrier;
+// verdict round 3 item 4).
 // ABL: ablation bits for tools/attn_tune timing studies only (product launches use 0; results
 // are wrong with any bit set): 1 every tile full and unmasked for every block (no causal
 // structure), 2 p = s (no exp), 4 no K/V loads after tile 0, 8 no barrier in the tile loop,
@@ -194,6 +196,18 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
                     }
                 }
                 if constexpr ((ABL & (64 | 128)) != 0) __builtin_amdgcn_s_setprio(0);
+                // ABL & 2048 (unmasked body): the score phase hand-ordered — K fragment reads
+                // (ds_read_b128) two fragments ahead of their 4 MFMAs, the phase fenced off
+                if constexpr ((ABL & 2048) != 0 && !MASKED) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS reads, two fragments ahead
+#pragma unroll
+                    for (int i = 0; i < KG * ND - 2; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 // causal mask + tile max; lane holds keys k0 + kg*16 + fk + r for query q_abs
                 float mt = -INFINITY;
 #pragma unroll
@@ -230,6 +244,7 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
                 for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;
                 }
                 if constexpr ((ABL & (64 | 256)) != 0) __builtin_amdgcn_s_setprio(1);
+                if constexpr ((ABL & 4096) != 0 && !MASKED) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int kg = 0; kg < KG; ++kg) {
                     if (!live[kg]) continue;
@@ -240,6 +255,17 @@ __global__ void __launch_bounds__(256, 2) attn_research_kernel(AttnArgs p) {
                             const float vf = Vs[cur][kg * 16 + fk + s][dg * 16 + fq];
                             o[j][dg] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf, sacc[kg][s], o[j][dg], 0, 0, 0);
                         }
+                }
+                // ABL & 4096 (unmasked body): the P.V phase hand-ordered — V reads (ds_read_b32) two
+                // MFMAs ahead: 2 reads, then (1 read, 1 MFMA) pairs, then the last 2 MFMAs
+                if constexpr ((ABL & 4096) != 0 && !MASKED) {
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+#pragma unroll
+                    for (int i = 0; i < KG * ND * 4 - 2; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x008, 2, 1);
                 }
                 if constexpr ((ABL & (64 | 256)) != 0) __builtin_amdgcn_s_setprio(0);
             };

@@ -184,6 +184,12 @@ int main(int argc, char** argv) {
             rounds, iters);
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "sched") {  // hand-ordered score / P.V phases
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AABL(2048), AABL(4096), AABL(2048 | 4096), AVAR(48, 4, 1, 64)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M chunk L=200 at start_pos 37", 64, 200, 6, 6, 48, v, 1, 1, 37);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "prio") {  // s_setprio around the MFMA clusters
         std::vector<Variant> v = {AVAR(48, 4, 1, 64), AABL(64), AABL(128), AABL(256), AVAR(48, 4, 1, 64)};
         run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
