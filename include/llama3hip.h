@@ -200,7 +200,9 @@ int l3_kernel_stats(l3_ctx* ctx, double* total_ms, int64_t* count);
 int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits);
 /* Whether the captured batch-1 decode step is the persistent kernel (one launch per greedy step,
  * decode_persist.hip: every layer, the lm_head and the argmax with in-launch hand-offs) rather
- * than the 25-kernel graph; env L3_DECODE_PERSIST (read at capture) picks it. */
+ * than the 25-kernel graph.  The persistent step is the default for shapes it takes (HD <= 64,
+ * decode_persist_ok); env L3_DECODE_PERSIST (read at capture): 1 default, 2 layer stages on one
+ * XCD, 0 the graph. */
 int l3_decode_persistent(l3_ctx* ctx, int32_t* active);
 /* Lazy greedy decode runs up to 16 steps ahead of the caller on the device (undone if the
  * caller leaves the schedule, so results are unchanged), and at most ~4 ms of decode work by

@@ -50,15 +50,13 @@ __device__ __forceinline__ u64 gget(u64* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // XCD-local hand-offs (DecodePersistArgs::xcd: every producer and consumer on one XCD, sharing its
-// L2): the store lands in the L2 (the CU's L1 is write-through), the load misses the L1 (sc0) and
-// reads the L2 — no trip through the MALL as the agent-scope (sc1) pair takes.  The load is a
-// buffer load so that the compiler still counts it (vmcnt) like any other.
+// L2): the granule store stops at that L2 (workgroup scope: no sc1 write-through to memory) and the
+// consumers' agent-scope loads find it there.  tools/handoff_xcd, 32 workgroups on one XCD: 1.0 us
+// per all-to-all edge against 1.73 with the write-through store (2.63 over all 8 XCDs); the
+// load forms that stop at the L1 or L2 of their own (sc0, L1 invalidate + plain load) never saw
+// the stores and timed out.  Only for consumers on the producer's XCD.
 __device__ __forceinline__ void gput_xcd(u64* g, unsigned tag, float v) {
     __hip_atomic_store(g, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ u64 gget_xcd(__amdgpu_buffer_rsrc_t r, int i) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, i * 8, 0, 1);  // aux 1: sc0
-    return (u64)(unsigned)v[0] | ((u64)(unsigned)v[1] << 32);
 }
 template <bool LOCAL>
 __device__ __forceinline__ void gput_s(u64* g, unsigned tag, float v) {
@@ -96,20 +94,16 @@ __device__ __forceinline__ void give_up(const Ctx& c) {
 // granules g[idx(i)] for i < n into dst[i] (LDS), every thread its i = tid + NT*k, all of a
 // thread's loads in flight per pass; re-read until every tag is the launch's.  Ends with a
 // workgroup barrier; false if this workgroup gave up (caller returns).
-template <int PER, bool LOCAL, typename Idx>
+template <int PER, typename Idx>
 __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
     const int tid = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 0x7fffffff, 0x00020000);
     bool ok = false;
     for (unsigned spin = 0;; ++spin) {
         ok = true;
         u64 x[PER];
         // unpredicated (a clamped index past n: a predicated load is a branch that waits)
 #pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = idx(min(tid + NT * k, n - 1));
-            x[k] = LOCAL ? gget_xcd(r, i) : gget(g + i);
-        }
+        for (int k = 0; k < PER; ++k) x[k] = gget(g + idx(min(tid + NT * k, n - 1)));
 #pragma unroll
         for (int k = 0; k < PER; ++k) ok &= (unsigned)(x[k] >> 32) == c.tag;
         if (ok) {
@@ -131,11 +125,11 @@ __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, I
     return !*c.bad;
 }
 
-template <bool LOCAL, typename Idx>
+template <typename Idx>
 __device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
-    if (n <= NT) return sweep<1, LOCAL>(c, g, n, dst, idx, sleep);
-    if (n <= 2 * NT) return sweep<2, LOCAL>(c, g, n, dst, idx, sleep);
-    return sweep<4, LOCAL>(c, g, n, dst, idx, sleep);  // n <= 1024 (eligibility)
+    if (n <= NT) return sweep<1>(c, g, n, dst, idx, sleep);
+    if (n <= 2 * NT) return sweep<2>(c, g, n, dst, idx, sleep);
+    return sweep<4>(c, g, n, dst, idx, sleep);  // n <= 1024 (eligibility)
 }
 
 // block sum of one value per thread (every thread gets it)
@@ -274,12 +268,48 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     // the generate-history fields workgroup 0 writes at the end, fetched now (off the final path)
     const int hist_base = p.st->hist_base, hist_cap = p.st->hist_cap;
     int32_t* const hist = p.st->hist;
-    // XL: a layer workgroup off the expected XCD would never see its peers' XCD-local stores —
-    // give up at once (the host checked the placement once, l3::decode_persist_xcd_probe)
-    if (XL && layer_wg && xcc_id() != p.xcc) {
-        if (tid == 0) give_up(c);
-        goto done;
-    }
+    // from_parts: the previous step (the launch before this one in the same graph) left its
+    // lm_head partials and no id; every layer workgroup reduces them itself (plain loads: written
+    // by the previous launch) — its final argmax hand-off and reduction come off that step's tail.
+    // This launch's own partials overwrite them only after every layer workgroup has started
+    // (the lm stage waits for the whole layer chain, which needs every layer workgroup).
+    // (called before layer 0's W rows are requested: called after them, in stage A, the
+    // partials' loads waited for the W rows in the in-order memory counter and the step measured
+    // 0.088-0.089 against 0.086 ms)
+    auto reduce_parts = [&]() {
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < nlm; i += NT) {
+            const u64 v = lm_g[2 * i], x = lm_g[2 * i + 1];
+            const float bv = __uint_as_float((unsigned)v);
+            const int ix = (int)(unsigned)x;
+            const bool take = argmax_better(bv, ix, best, bi);
+            best = take ? bv : best;
+            bi = take ? ix : bi;
+        }
+        group_argmax<64>(best, bi, tid & 63);
+        __shared__ float pb[4];
+        __shared__ int pi[4];
+        if ((tid & 63) == 0) { pb[tid >> 6] = best; pi[tid >> 6] = bi; }
+        lds_barrier();
+        best = pb[0];
+        bi = pi[0];
+        for (int w2 = 1; w2 < 4; ++w2) {
+            const bool take = argmax_better(pb[w2], pi[w2], best, bi);
+            best = take ? pb[w2] : best;
+            bi = take ? pi[w2] : bi;
+        }
+        id = bi;
+        if (lw == 0 && tid == 0) {  // the previous step's id: its generate history entry
+            const int q = pos - 1 - hist_base;
+            if (hist && q >= 0 && q < hist_cap) hist[q] = id;
+        }
+    };
+    // XL relies on wg % 8 == 0 sharing one XCD (round-robin dealing; which XCD varies from launch
+    // to launch; the host checked the dealing once, l3::decode_persist_xcd_probe): were a layer
+    // workgroup elsewhere, its peers' XCD-local stores would not reach it and the bounded waits
+    // would end the launch with the error word set
+    if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 128 + 127] = xcc_id();
     if (!layer_wg) {
         // ---- final RMSNorm + lm_head (llama3.py:304-307) + this workgroup's argmax (:320) ---------
         f32x4 lw[LMPF][1][NCD];  // live on this path only (not across the layer loop)
@@ -296,7 +326,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 __builtin_amdgcn_s_sleep(16);
             }
         }
-        if (!sweep_n<false>(c, g_last, D, xs, [](int i) { return i; }, 8)) goto done;
+        if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, 8)) goto done;
         stamp(100);
         const float rs = inv_rms(c, xs, D);
         stamp(103);
@@ -339,41 +369,8 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         goto done;
     }
 
-    // from_parts: the previous step (the launch before this one in the same graph) left its
-    // lm_head partials and no id; every layer workgroup reduces them itself (plain loads: written
-    // by the previous launch) — its final argmax hand-off and reduction come off that step's tail.
-    // This launch's own partials overwrite them only after every layer workgroup has started
-    // (the lm stage waits for the whole layer chain, which needs every layer workgroup).
-    if (p.from_parts) {  // (layer workgroups only from here on)
-        float best = -INFINITY;
-        int bi = 0x7fffffff;
-        for (int i = tid; i < nlm; i += NT) {
-            const u64 v = lm_g[2 * i], x = lm_g[2 * i + 1];
-            const float bv = __uint_as_float((unsigned)v);
-            const int ix = (int)(unsigned)x;
-            const bool take = argmax_better(bv, ix, best, bi);
-            best = take ? bv : best;
-            bi = take ? ix : bi;
-        }
-        group_argmax<64>(best, bi, tid & 63);
-        __shared__ float pb[4];
-        __shared__ int pi[4];
-        if ((tid & 63) == 0) { pb[tid >> 6] = best; pi[tid >> 6] = bi; }
-        lds_barrier();
-        best = pb[0];
-        bi = pi[0];
-        for (int w2 = 1; w2 < 4; ++w2) {
-            const bool take = argmax_better(pb[w2], pi[w2], best, bi);
-            best = take ? pb[w2] : best;
-            bi = take ? pi[w2] : bi;
-        }
-        id = bi;
-        if (lw == 0 && tid == 0) {  // the previous step's id: its generate history entry
-            const int q = pos - 1 - hist_base;
-            if (hist && q >= 0 && q < hist_cap) hist[q] = id;
-        }
-    }
 
+    if (p.from_parts) reduce_parts();
     for (int li = 0; li < p.n_layers; ++li) {
         u64* g_qkv = p.gran + slab * li;
         u64* g_o = g_qkv + qkvn;
@@ -383,9 +380,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         const float* wqkv = p.wqkv[li];
         float* ck = p.cache_k[li];
         float* cv = p.cache_v[li];
-        // the attention workgroups' K / V rows of this layer (keys before pos: written by earlier
-        // launches) go out first, at the layer's start: they come from the MALL / HBM (~1 us),
-        // which the QKV stage and its hand-off now cover (issued after it, stage B waited on them)
+        // the attention workgroup's K / V rows of this layer (keys before pos: written by earlier
+        // launches), fetched in stage B before its hand-off wait (fetched at the layer's start
+        // instead, ahead of the QKV rows, the step measured 0.091 against 0.087 ms)
         const int kvh = lw / (H / KVH);
         const int D4 = HD / 4, R = NT / D4;  // PV: R key groups x D4 float4 columns
         const int rg = tid / D4, d4 = tid - rg * D4;
@@ -397,12 +394,6 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         const int kmax = pos > 0 ? pos - 1 : 0;
         const gf4p Kg = gf4(K4p), Vg = gf4(V4p);
         f32x4 kr[KPF], vr[VPF];
-        if (lw < H) {
-#pragma unroll
-            for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
-#pragma unroll
-            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + min(d4, D4 - 1)];
-        }
         // ---- stage A: RMSNorm + QKV + RoPE + KV append (llama3.py:248, 166-185) -------------
         {
             bool valid;
@@ -428,7 +419,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             if (li == 0) {
                 for (int i = tid; i < D; i += NT) hin[i] = p.emb[(int64_t)id * D + i];
                 lds_barrier();
-            } else if (!sweep_n<XL>(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
+            } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
                 goto done;
             }
             stamp(1 + 10 * li);
@@ -455,7 +446,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int h = lw;
             float* qs = xs;                              // q | k_new | v_new of this head
             const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
-            if (!sweep_n<XL>(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
+#pragma unroll
+            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + min(d4, D4 - 1)];
+            if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
                 goto done;
             stamp(3 + 10 * li);
 #pragma unroll
@@ -548,7 +543,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int row[1] = {u};
             f32x4 w[1][NCD];
             load_rows<1, NCD>(p.wo[li], row, K4q, valid, w);
-            if (!sweep_n<XL>(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
+            if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
             stamp(5 + 10 * li);
             float acc[1];
             dot_rows<1, NCD>(w, xs, K4q, acc);
@@ -570,7 +565,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             }
             f32x4 w[2 * GU][NCD];
             load_rows<2 * GU, NCD>(p.wgu[li], row, K4d, valid, w);
-            if (!sweep_n<XL>(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
+            if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
             stamp(7 + 10 * li);
             const float rs = inv_rms(c, h1s, D);
             float acc[2 * GU];
@@ -591,7 +586,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int row[1] = {u};
             f32x4 w[1][NCF];
             load_rows<1, NCF>(p.wd[li], row, K4f, valid, w);
-            if (!sweep_n<XL>(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
+            if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
             stamp(9 + 10 * li);
             float acc[1];
             dot_rows<1, NCF>(w, xs, K4f, acc);
@@ -613,7 +608,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     // ---- workgroup 0, last step of a graph: the step's greedy id from the lm partials; generate history, position ----
     {
         float* pv = xs;  // [2 nlm]
-        if (sweep_n<false>(c, lm_g, 2 * nlm, pv, [](int i) { return i; })) {
+        if (sweep_n(c, lm_g, 2 * nlm, pv, [](int i) { return i; })) {
             stamp(105);
             float best = -INFINITY;
             int bi = 0x7fffffff;

@@ -11,7 +11,7 @@ namespace l3 {
 //   runtime.hip  L3_BATCH_SPLIT (2), L3_LAST_LAYER_ALL_ROWS (0), L3_DECODE_FUSE_O (1),
 //                L3_LM_AMAX (1), L3_DECODE_FOLD_ARGMAX (1), L3_DECODE_SPECULATE (1), L3_DECODE_GRAPH_STEPS (8),
 //                L3_DECODE_GRAPH (1), L3_COMM_MODE (1), L3_COMM_PRIORITY (1), L3_GROUP_MULTI_PATH (0),
-//                L3_DECODE_PERSIST (0; 1 all-XCD layout, 2 one-XCD layout)
+//                L3_DECODE_PERSIST (1 all-XCD layout; 2 one-XCD layout, 0 graph)
 //   gemm.hip     L3_SPLITK (1), L3_SPLITK_CFG (0), L3_SPLITK_BLOCKS (1024), L3_SPLITK_MINKT (8),
 //                L3_GEMV_NT (1), L3_GEMV_LPU (0 = by shape), L3_GEMV_MR (by shape), L3_SKINNY (1),
 //                L3_SKINNY_MIN (9)

@@ -955,13 +955,13 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
     return 0;
 }
 
-// Persistent batch-1 decode step (decode_persist.hip): L3_DECODE_PERSIST=1 (layer stages on 64
-// workgroups over all XCDs) or 2 (on the 32 workgroups of one XCD, if the placement probe agrees;
-// else 1), and a shape the kernel takes (decode_persist_ok).  Its buffers are made once, with the
+// Persistent batch-1 decode step (decode_persist.hip; the default): L3_DECODE_PERSIST=1 (layer
+// stages on 64 workgroups over all XCDs), 2 (on the 32 workgroups of one XCD, if the placement
+// probe agrees; else 1) or 0 (the 25-kernel graph), and a shape the kernel takes (decode_persist_ok).  Its buffers are made once, with the
 // stream idle.
 static bool persist_wanted(l3_ctx* c, int B) {
     // read at every capture (captures are rare), so a process can A/B the paths
-    const int mode = env_knob("L3_DECODE_PERSIST", 0);
+    const int mode = env_knob("L3_DECODE_PERSIST", 1);
     if (!mode || B != 1 || c->layers.empty() || !c->dec_state) return false;
     if (mode == 2 && c->persist_xcd_ok < 0) c->persist_xcd_ok = decode_persist_xcd_probe(&c->persist_xcc);
     DecodePersistArgs a{};

@@ -1141,18 +1141,20 @@ def test_persistent_decode_step_matches_golden(tmpdir_mod, monkeypatch, preset):
     against the reference's own 145 greedy ids of "I have a dream" (llama3.py:310-321, the
     decode hole included): the device loop (8-step graphs, the inner steps leaving their argmax to
     the next launch), the lazy generator with run-ahead, and a second generate on the caches the
-    first left behind, each bit-exact; and the graph path (L3_DECODE_PERSIST=0) still taken."""
+    first left behind, each bit-exact — in both layouts (1: layer stages on 64 workgroups over all
+    XCDs, the default; 2: on the 32 workgroups of one XCD) — and the 25-kernel graph path
+    (L3_DECODE_PERSIST=0) still taken."""
     g = load_golden(f"stories15m_{preset}")
     args = synth.stories15m(1)
     _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, int(g["seed"]), preset)
     prompt = np.asarray(g["dream_prompt"]).reshape(1, -1)
     want = np.asarray(g["dream_ids"]).reshape(1, -1)
     n = int(g["dream_max_new"])
-    for on in ("1", "0"):
+    for on in ("1", "2", "0"):
         monkeypatch.setenv("L3_DECODE_PERSIST", on)
         m = llama3.Llama(path, args)
         np.testing.assert_array_equal(m.generate_all(prompt, n), want)
-        assert m.context.decode_persistent() == (on == "1")
+        assert m.context.decode_persistent() == (on != "0")
         lazy = np.concatenate(list(m.generate(prompt, n)), axis=1)
         np.testing.assert_array_equal(lazy, want)
         # an abandoned generator (run-ahead steps undone), then a full one

@@ -4,9 +4,8 @@
 // granules and re-reads all V until every tag matches (bounded spins, *tmo on timeout).
 //   mode 0 (agent): agent-scope relaxed atomic stores / loads (sc1: through L2 to the MALL),
 //                   participants = every workgroup (stride 1) or wg % 8 == 0 (stride 8)
-//   mode 1 (xcd):   plain stores (land in the XCD's L2) and sc0 buffer loads (miss L1, hit L2);
-//                   participants = wg % 8 == 0, which round-robin dispatch puts on one XCD —
-//                   checked: every participant records HW_REG_XCC_ID, the host requires one value
+//   modes 1-4 (below): store / load pairs for participants wg % 8 == 0, which round-robin
+//                   dispatch puts on one XCD — each participant records HW_REG_XCC_ID
 // The grid is 256 workgroups (one per CU); non-participants leave at once.
 //   Build: make -C tools handoff_xcd ; run: tools/handoff_xcd
 #include <hip/hip_runtime.h>
@@ -25,16 +24,23 @@
 
 typedef unsigned long long u64;
 
+// MODE 0: agent-scope store + agent-scope load (sc1 both)
+// MODE 1: workgroup-scope store (lands in the XCD's L2) + sc0 buffer load (found NOT to see it:
+//         timeout — a group-scope load may hit the CU's L1)
+// MODE 2: workgroup-scope store + L1 invalidate (buffer_inv sc0) + plain load per poll round
+// MODE 3: workgroup-scope store + agent-scope load
+// MODE 4: agent-scope store + L1 invalidate + plain load
 template <int MODE>
 __device__ __forceinline__ void put(u64* g, unsigned tag, float v) {
     const u64 x = ((u64)tag << 32) | __float_as_uint(v);
-    if (MODE == 0) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MODE == 0 || MODE == 4) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 template <int MODE>
 __device__ __forceinline__ u64 get(u64* base, __amdgpu_buffer_rsrc_t r, int idx) {
-    if (MODE == 0) return __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MODE == 0 || MODE == 3) return __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MODE == 2 || MODE == 4) return __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, 1);  // sc0: miss L1
     return (u64)(unsigned)v[0] | ((u64)(unsigned)v[1] << 32);
 }
@@ -65,6 +71,7 @@ __global__ void __launch_bounds__(256) chain_kernel(u64* buf, int E, int V, int 
         for (unsigned spin = 0; !ok; ++spin) {
             ok = true;
             u64 x[PER];
+            if (MODE == 2 || MODE == 4) asm volatile("buffer_inv sc0" ::: "memory");  // drop this CU's L1 lines
 #pragma unroll
             for (int k = 0; k < PER; ++k) x[k] = get<MODE>(g, r, min(tid + 256 * k, V - 1));
 #pragma unroll
@@ -113,7 +120,8 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     struct Cfg { int mode, stride; const char* name; } cfgs[] = {
-        {0, 1, "agent, all 256 wgs"}, {0, 8, "agent, wg%8==0 (32)"}, {1, 8, "xcd-L2, wg%8==0 (32)"}};
+        {0, 1, "agent, all 256 wgs"}, {0, 8, "agent, wg%8==0 (32)"}, {2, 8, "wg st, inv+ld (32)"},
+        {3, 8, "wg st, agent ld (32)"}, {4, 8, "agent st, inv+ld (32)"}, {1, 8, "wg st, sc0 ld (32)"}};
     for (const Cfg& cf : cfgs)
         for (int V : Vs) {
             double us[2];
@@ -121,19 +129,22 @@ int main() {
                 const int edges = which ? E : 0;
                 auto launch = [&]() {
                     CK(hipMemsetAsync(buf, 0, (size_t)E * V * 8, s));
-                    if (cf.mode == 0)
-                        hipLaunchKernelGGL((chain_kernel<4, 0>), dim3(grid), dim3(256), 0, s, buf, edges, V, cf.stride, out, tmo, xcc);
-                    else
-                        hipLaunchKernelGGL((chain_kernel<4, 1>), dim3(grid), dim3(256), 0, s, buf, edges, V, cf.stride, out, tmo, xcc);
+                    switch (cf.mode) {
+#define CASE(M) case M: hipLaunchKernelGGL((chain_kernel<4, M>), dim3(grid), dim3(256), 0, s, buf, edges, V, cf.stride, out, tmo, xcc); break;
+                        CASE(0) CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+                    }
                 };
                 CK(hipMemset(xcc, 0, 256 * 4));
                 for (int r = 0; r < 20; ++r) launch();
                 CK(hipStreamSynchronize(s));
                 unsigned t0 = 0;
                 CK(hipMemcpy(&t0, tmo, 4, hipMemcpyDeviceToHost));
-                if (t0) {  // the hand-off never completed (participants not sharing an L2?): stop here
+                if (t0) {  // the hand-off never completed: the next configs still run
                     printf("%-22s V=%4d: TIMEOUT in warm-up, not timed\n", cf.name, V);
-                    return 1;
+                    CK(hipMemset(tmo, 0, 4));
+                    us[0] = us[1] = -1;
+                    break;
                 }
                 const int reps = 200;
                 CK(hipEventRecord(e0, s));
@@ -144,6 +155,7 @@ int main() {
                 CK(hipEventElapsedTime(&ms, e0, e1));
                 us[which] = ms * 1e3 / reps;
             }
+            if (us[0] < 0) continue;
             unsigned t = 0, x[256];
             CK(hipMemcpy(&t, tmo, 4, hipMemcpyDeviceToHost));
             CK(hipMemcpy(x, xcc, sizeof x, hipMemcpyDeviceToHost));

@@ -27,10 +27,14 @@ if "--read" not in sys.argv:
         m = llama3.Llama(p, args)
     m.generate_all(np.array([[1, 76, 505, 263, 12561]]), 150)
 st = np.fromfile(path, dtype=np.uint64).reshape(256, 128).astype(np.int64)
+xcc = st[:, 127].copy()
+st[:, 127] = 0
 t0 = st[:, 0][st[:, 0] > 0].min()
 us = lambda x: (x - t0) / 100.0  # noqa: E731
-names = ["qkv", "attn+o", "oproj", "gateup", "down"]  # (the O-proj rides in attention)
-lay = st[:64]
+names = ["qkv", "attn", "oproj", "gateup", "down"]
+lay_idx = np.nonzero(st[:, 1] > 0)[0]  # layer workgroups (0..63, or wg % 8 == 0 in the one-XCD layout)
+lm_idx = np.setdiff1d(np.arange(256), lay_idx)
+lay = st[lay_idx]
 
 
 def span(rows, k):
@@ -48,11 +52,12 @@ for li in range(6):
         arr = f"{a0:7.2f}..{a1:7.2f}" if a0 is not None else " " * 16
         print(f"  L{li} {names[k]:6s} in {arr}  out {p0:7.2f}..{p1:7.2f}")
 for k, nm in ((0, "start"), (100, "lm input"), (103, "lm rms"), (104, "lm rows done"), (101, "lm partial")):
-    a = span(st[:64], k)
-    b = span(st[64:], k)
+    a = span(lay, k)
+    b = span(st[lm_idx], k)
     print(f"  {nm:12s} layer wgs {a[0]}..{a[1]}   lm wgs {b[0]}..{b[1]}")
-print("attention workgroups, layer 1: in / scores / max / sum / PV / part stored / O-proj partials / out")
+print("attention workgroups, layer 1: in / scores / max / sum / PV / part stored / out")
 for h in range(6):
-    print("  head", h, " ".join(f"{us(st[h, k]):7.2f}" for k in (13, 110, 111, 112, 113, 114, 115, 14)))
+    print("  head", h, " ".join(f"{us(st[lay_idx[h], k]):7.2f}" for k in (13, 110, 111, 112, 113, 114, 14)))
+print("layer workgroups' XCDs:", sorted(set(xcc[lay_idx].tolist())), " lm workgroups' XCDs:", sorted(set(xcc[lm_idx].tolist())))
 for k, nm in ((105, "wg0 partials in"), (102, "greedy id")):
     print(f"  {nm}: {us(st[0, k]):.2f}")
