@@ -164,38 +164,40 @@ typedef const __attribute__((address_space(1))) f32x4* gf4p;
 __device__ __forceinline__ gf4p gf4(const void* p) { return (gf4p)(p); }
 
 // W rows of one unit into registers: lane j of the unit holds float4s k4 = j + LPR * t, t < NC.
-// Unpredicated loads from clamped (in-bounds) addresses, zeroed afterwards where they fall past
-// K or the unit is not valid: a predicated load compiles to an exec-masked branch that waits for
-// every load in flight before the next one is issued (one round trip per float4)
+// Unpredicated loads from clamped (in-bounds) addresses: a predicated load compiles to an
+// exec-masked branch that waits for every load in flight before the next one is issued (one round
+// trip per float4).  Nothing is zeroed here: the chunks past K meet zeroed x chunks in the dot
+// (read_x), and an invalid unit's (clamped, finite) rows give a result nobody publishes — zeroing
+// the rows cost a v_cndmask per element of W after the loads landed, on every stage
 template <int ROWS, int NC>
-__device__ __forceinline__ void load_rows(const float* W, const int (&row)[ROWS], int K4, bool valid,
-                                          f32x4 (&w)[ROWS][NC]) {
+__device__ __forceinline__ void load_rows(const float* W, const int (&row)[ROWS], int K4, f32x4 (&w)[ROWS][NC]) {
     const int j = threadIdx.x % LPR;
     const gf4p W4 = gf4(W);
 #pragma unroll
     for (int t = 0; t < NC; ++t) {
-        const int k4 = j + LPR * t, kk = min(k4, K4 - 1);
+        const int kk = min(j + LPR * t, K4 - 1);
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) w[r][t] = W4[(int64_t)row[r] * K4 + kk];
     }
-#pragma unroll
-    for (int t = 0; t < NC; ++t) {
-        const bool in = valid && j + LPR * t < K4;
-#pragma unroll
-        for (int r = 0; r < ROWS; ++r) w[r][t] = in ? w[r][t] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
 }
 
-// branch-free: every chunk's LDS read is issued before the first FMA (x read at a clamped index
-// past K meets a zeroed W chunk); a per-chunk bound check compiled to a branch and an LDS wait
-// per chunk (the lm_head's eight passes took 3 us)
-template <int ROWS, int NC>
-__device__ __forceinline__ void dot_rows(const f32x4 (&w)[ROWS][NC], const float* x, int K4, float (&acc)[ROWS]) {
+// x chunks of this lane (LDS), zero past K
+template <int NC>
+__device__ __forceinline__ void read_x(const float* x, int K4, f32x4 (&xv)[NC]) {
     const int j = threadIdx.x % LPR;
     const f32x4* X4 = reinterpret_cast<const f32x4*>(x);
-    f32x4 xv[NC];
 #pragma unroll
     for (int t = 0; t < NC; ++t) xv[t] = X4[min(j + LPR * t, K4 - 1)];
+#pragma unroll
+    for (int t = 0; t < NC; ++t) xv[t] = j + LPR * t < K4 ? xv[t] : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+// branch-free: every chunk's LDS read is issued before the first FMA; a per-chunk bound check
+// compiled to a branch and an LDS wait per chunk (the lm_head's eight passes took 3 us)
+template <int ROWS, int NC>
+__device__ __forceinline__ void dot_rows(const f32x4 (&w)[ROWS][NC], const float* x, int K4, float (&acc)[ROWS]) {
+    f32x4 xv[NC];
+    read_x<NC>(x, K4, xv);
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
 #pragma unroll
@@ -205,6 +207,15 @@ __device__ __forceinline__ void dot_rows(const f32x4 (&w)[ROWS][NC], const float
             acc[r] += w[r][t].x * xv[t].x + w[r][t].y * xv[t].y + w[r][t].z * xv[t].z + w[r][t].w * xv[t].w;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) acc[r] = group_sum<LPR>(acc[r]);
+}
+
+// one row's dot with x already in registers (read_x): the lm_head's passes share one x
+template <int NC>
+__device__ __forceinline__ float dot_row_x(const f32x4 (&w)[NC], const f32x4 (&xv)[NC]) {
+    float acc = 0.f;
+#pragma unroll
+    for (int t = 0; t < NC; ++t) acc += w[t].x * xv[t].x + w[t].y * xv[t].y + w[t].z * xv[t].z + w[t].w * xv[t].w;
+    return acc;
 }
 
 // this workgroup's unit range of a layer stage with n units over GL workgroups (one pass: the
@@ -317,7 +328,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         for (int ps = 0; ps < LMPF; ++ps) {  // nothing else to do: the rows land while the layers run
             const int r = lm_r0 + ps * UPP + tid / LPR;
             const int row[1] = {min(r, p.VS - 1)};
-            load_rows<1, NCD>(p.lm_head, row, K4d, ps < lm_passes && r < lm_r1, lw[ps]);
+            load_rows<1, NCD>(p.lm_head, row, K4d, lw[ps]);  // clamped rows
         }
         u64* g_last = p.gran + slab * (p.n_layers - 1) + h2_off;
         if (tid == 0) {  // a long wait: one lane polls the last granule, sleeping
@@ -338,17 +349,33 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             best = take ? v : best;
             bi = take ? r : bi;
         };
+        // the passes held in registers since the launch: x read from LDS once for all of them (a
+        // dot_rows per pass re-read it: 11 x 20 KB of LDS traffic per workgroup), the LPR-lane sums
+        // after all the dots (independent chains)
+        f32x4 xv[NCD];
+        read_x<NCD>(xs, K4d, xv);
+        float lacc[LMPF];
 #pragma unroll
-        for (int ps = 0; ps < LMPF; ++ps) {  // the passes held in registers since the launch
-            float acc[1];
-            dot_rows<1, NCD>(lw[ps], xs, K4d, acc);
-            consider(lm_r0 + ps * UPP + tid / LPR, acc[0]);
+        for (int ps = 0; ps < LMPF; ++ps) lacc[ps] = dot_row_x<NCD>(lw[ps][0], xv);
+#pragma unroll
+        for (int ps = 0; ps < LMPF; ++ps) lacc[ps] = group_sum<LPR>(lacc[ps]);
+        // this lane's rows rise with the pass, so "strictly greater, or the first NaN" in pass
+        // order is argmax_better (first index on ties, NaN first) without its index compares and
+        // branches (the eleven branchy compares and the zeroing of the rows were ~3 us of VALU)
+#pragma unroll
+        for (int ps = 0; ps < LMPF; ++ps) {
+            const int r = lm_r0 + ps * UPP + tid / LPR;
+            const float v = lacc[ps] * rs;
+            const bool vn = v != v, bn = best != best;
+            const bool take = r < lm_r1 && (bi == 0x7fffffff || v > best || (vn && !bn));
+            best = take ? v : best;
+            bi = take ? r : bi;
         }
         for (int ps = LMPF; ps < lm_passes; ++ps) {  // rows past them, streamed now
             const int r = lm_r0 + ps * UPP + tid / LPR;
             f32x4 w[1][NCD];
             const int row[1] = {min(r, p.VS - 1)};
-            load_rows<1, NCD>(p.lm_head, row, K4d, r < lm_r1, w);
+            load_rows<1, NCD>(p.lm_head, row, K4d, w);
             float acc[1];
             dot_rows<1, NCD>(w, xs, K4d, acc);
             consider(r, acc[0]);
@@ -400,7 +427,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int u = stage_unit(p, qkvn / 2, lw, valid);  // RoPE pair (rows 2u, 2u + 1)
             const int row[2] = {2 * u, 2 * u + 1};
             f32x4 w[2][NCD];
-            load_rows<2, NCD>(wqkv, row, K4d, valid, w);
+            load_rows<2, NCD>(wqkv, row, K4d, w);
             const int col = 2 * u;
             const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
             const int cc = col - (sec == 0 ? 0 : sec == 1 ? qdim : qdim + kvdim);
@@ -542,7 +569,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int u = stage_unit(p, D, lw, valid);
             const int row[1] = {u};
             f32x4 w[1][NCD];
-            load_rows<1, NCD>(p.wo[li], row, K4q, valid, w);
+            load_rows<1, NCD>(p.wo[li], row, K4q, w);
             if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
             stamp(5 + 10 * li);
             float acc[1];
@@ -564,7 +591,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 row[2 * g + 1] = row[2 * g] + 16;
             }
             f32x4 w[2 * GU][NCD];
-            load_rows<2 * GU, NCD>(p.wgu[li], row, K4d, valid, w);
+            load_rows<2 * GU, NCD>(p.wgu[li], row, K4d, w);
             if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
             stamp(7 + 10 * li);
             const float rs = inv_rms(c, h1s, D);
@@ -585,7 +612,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int u = stage_unit(p, D, lw, valid);
             const int row[1] = {u};
             f32x4 w[1][NCF];
-            load_rows<1, NCF>(p.wd[li], row, K4f, valid, w);
+            load_rows<1, NCF>(p.wd[li], row, K4f, w);
             if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
             stamp(9 + 10 * li);
             float acc[1];
