@@ -480,10 +480,14 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
                 goto done;
             stamp(3 + 10 * li);
+            // only the K chunks past HD need zeroing (the q4 reads there land in k_new); a lane's
+            // score past pos is never kept and a V row past pos never used (P.V checks k < pos),
+            // so nothing else is masked — a select per element was ~100 VALU on this critical path
+            if (D4 < KPF) {  // uniform: none for HD = 4 KPF (stories15M)
 #pragma unroll
-            for (int i = 0; i < KPF; ++i) kr[i] = (i < D4 && tid < pos) ? kr[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int t = 0; t < VPF; ++t) vr[t] = (rg < R && rg + t * R < pos) ? vr[t] : f32x4{0.f, 0.f, 0.f, 0.f};
+                for (int i = 0; i < KPF; ++i)
+                    if (i >= D4) kr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
             const f32x4* q4 = reinterpret_cast<const f32x4*>(qs);
             const f32x4* kn4 = reinterpret_cast<const f32x4*>(qs + HD);
             const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
@@ -531,11 +535,13 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             if (li == 1) stamp(112);
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             if (rg < R) {
+                // every p read first (clamped index), then the FMAs with p zeroed past pos: a
+                // predicated read per key was a branch and an LDS wait per key
+                float pk[VPF];
 #pragma unroll
-                for (int t = 0; t < VPF; ++t) {
-                    const int k = rg + t * R;
-                    if (k < pos) acc += sc[k] * vr[t];
-                }
+                for (int t = 0; t < VPF; ++t) pk[t] = sc[min(rg + t * R, pos)];
+#pragma unroll
+                for (int t = 0; t < VPF; ++t) acc += (rg + t * R < pos ? pk[t] : 0.f) * vr[t];
                 for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
                 if (pos % R == rg) acc += sc[pos] * vn4[d4];
             }
