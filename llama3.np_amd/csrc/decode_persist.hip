@@ -150,14 +150,6 @@ __device__ __forceinline__ float block_max(const Ctx& c, float v) {
     return fmaxf(fmaxf(c.red[0], c.red[1]), fmaxf(c.red[2], c.red[3]));
 }
 
-// 1 / rms of the LDS vector x[0..n) (RMSNorm, llama3.py:111-114; the weight is folded into W)
-__device__ __forceinline__ float inv_rms(const Ctx& c, const float* x, int n) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < n; i += NT) s += x[i] * x[i];
-    s = block_sum(c, s);
-    return __builtin_amdgcn_rsqf(s / (float)n + c.p.eps);
-}
-
 // global (not flat) 16-byte loads: flat loads also count in lgkmcnt, so every LDS wait would
 // wait for them too
 typedef const __attribute__((address_space(1))) f32x4* gf4p;
@@ -207,6 +199,34 @@ __device__ __forceinline__ void dot_rows(const f32x4 (&w)[ROWS][NC], const float
             acc[r] += w[r][t].x * xv[t].x + w[r][t].y * xv[t].y + w[r][t].z * xv[t].z + w[r][t].w * xv[t].w;
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) acc[r] = group_sum<LPR>(acc[r]);
+}
+
+// 1 / rms of x from the chunks a 16-lane unit holds (read_x: together they cover x once), so no
+// workgroup reduction — inv_rms's block sum cost two barriers and a predicated loop per stage
+template <int NC>
+__device__ __forceinline__ float unit_inv_rms(const f32x4 (&xv)[NC], int n, float eps) {
+    float ss = 0.f;
+#pragma unroll
+    for (int t = 0; t < NC; ++t) ss += xv[t].x * xv[t].x + xv[t].y * xv[t].y + xv[t].z * xv[t].z + xv[t].w * xv[t].w;
+    ss = group_sum<LPR>(ss);
+    return __builtin_amdgcn_rsqf(ss / (float)n + eps);
+}
+// dot_rows plus the RMSNorm scale of x (RMSNorm, llama3.py:111-114; the weight is folded into W)
+template <int ROWS, int NC>
+__device__ __forceinline__ float dot_rows_rms(const f32x4 (&w)[ROWS][NC], const float* x, int K4, float eps,
+                                              float (&acc)[ROWS]) {
+    f32x4 xv[NC];
+    read_x<NC>(x, K4, xv);
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NC; ++t)
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r)
+            acc[r] += w[r][t].x * xv[t].x + w[r][t].y * xv[t].y + w[r][t].z * xv[t].z + w[r][t].w * xv[t].w;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) acc[r] = group_sum<LPR>(acc[r]);
+    return unit_inv_rms<NC>(xv, 4 * K4, eps);
 }
 
 // one row's dot with x already in registers (read_x): the lm_head's passes share one x
@@ -339,7 +359,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         }
         if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, 8)) goto done;
         stamp(100);
-        const float rs = inv_rms(c, xs, D);
+        f32x4 xv[NCD];
+        read_x<NCD>(xs, K4d, xv);
+        const float rs = unit_inv_rms<NCD>(xv, D, p.eps);
         stamp(103);
         float best = -INFINITY;
         int bi = 0x7fffffff;
@@ -352,8 +374,6 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         // the passes held in registers since the launch: x read from LDS once for all of them (a
         // dot_rows per pass re-read it: 11 x 20 KB of LDS traffic per workgroup), the LPR-lane sums
         // after all the dots (independent chains)
-        f32x4 xv[NCD];
-        read_x<NCD>(xs, K4d, xv);
         float lacc[LMPF];
 #pragma unroll
         for (int ps = 0; ps < LMPF; ++ps) lacc[ps] = dot_row_x<NCD>(lw[ps][0], xv);
@@ -450,9 +470,8 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 goto done;
             }
             stamp(1 + 10 * li);
-            const float rs = inv_rms(c, hin, D);
             float acc[2];
-            dot_rows<2, NCD>(w, hin, K4d, acc);
+            const float rs = dot_rows_rms<2, NCD>(w, hin, K4d, p.eps, acc);
             if (valid && tid % LPR == 0) {
                 const float v0 = acc[0] * rs, v1 = acc[1] * rs;
                 const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
@@ -600,9 +619,8 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             load_rows<2 * GU, NCD>(p.wgu[li], row, K4d, w);
             if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
             stamp(7 + 10 * li);
-            const float rs = inv_rms(c, h1s, D);
             float acc[2 * GU];
-            dot_rows<2 * GU, NCD>(w, h1s, K4d, acc);
+            const float rs = dot_rows_rms<2 * GU, NCD>(w, h1s, K4d, p.eps, acc);
             if (valid && tid % LPR == 0) {
 #pragma unroll
                 for (int g = 0; g < GU; ++g) {
