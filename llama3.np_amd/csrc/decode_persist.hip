@@ -132,22 +132,22 @@ __device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst,
     return sweep<4>(c, g, n, dst, idx, sleep);  // n <= 1024 (eligibility)
 }
 
-// block sum of one value per thread (every thread gets it)
-__device__ __forceinline__ float block_sum(const Ctx& c, float v) {
-    v = group_sum<64>(v);
-    const int tid = threadIdx.x;
-    lds_barrier();
-    if ((tid & 63) == 0) c.red[tid >> 6] = v;
-    lds_barrier();
-    return (c.red[0] + c.red[1]) + (c.red[2] + c.red[3]);
-}
+// block max / sum of one value per thread (every thread gets it), one barrier each: the two use
+// their own red slots (the attention stage calls max, then sum, once per layer; between two
+// uses of a slot every wave has passed other barriers, so its last reads are done)
 __device__ __forceinline__ float block_max(const Ctx& c, float v) {
     v = group_max<64>(v);
     const int tid = threadIdx.x;
-    lds_barrier();
     if ((tid & 63) == 0) c.red[tid >> 6] = v;
     lds_barrier();
     return fmaxf(fmaxf(c.red[0], c.red[1]), fmaxf(c.red[2], c.red[3]));
+}
+__device__ __forceinline__ float block_sum(const Ctx& c, float v) {
+    v = group_sum<64>(v);
+    const int tid = threadIdx.x;
+    if ((tid & 63) == 0) c.red[4 + (tid >> 6)] = v;
+    lds_barrier();
+    return (c.red[4] + c.red[5]) + (c.red[6] + c.red[7]);
 }
 
 // global (not flat) 16-byte loads: flat loads also count in lgkmcnt, so every LDS wait would
@@ -464,7 +464,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             // the layer input: the token's embedding row (llama3.py:287), else the previous
             // layer's output granules
             if (li == 0) {
-                for (int i = tid; i < D; i += NT) hin[i] = p.emb[(int64_t)id * D + i];
+                // one float4 per thread, one round trip (D / 4 <= NT by eligibility; a float per
+                // thread took two dependent trips for D > NT)
+                const gf4p E4 = gf4(p.emb + (int64_t)id * D);
+                const f32x4 e = E4[min(tid, K4d - 1)];
+                if (tid < K4d) reinterpret_cast<f32x4*>(hin)[tid] = e;
                 lds_barrier();
             } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
                 goto done;
@@ -550,7 +554,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 sc[k] = e;
                 l += e;
             }
-            l = block_sum(c, l);  // its barriers also publish sc
+            l = block_sum(c, l);  // its barrier also publishes sc
             if (li == 1) stamp(112);
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
             if (rg < R) {
@@ -700,7 +704,7 @@ bool decode_persist_ok(const DecodePersistArgs& a) {
     return a.D % 4 == 0 && a.FD % 4 == 0 && a.HD % 4 == 0 && a.HD >= 4 && a.HD <= 64 && a.H <= a.GL &&
            a.H % a.KVH == 0 && a.H * a.HD == a.D && ncd_of(a.D) && ncf_of(a.FD) && qkvn % 2 == 0 &&
            (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD / gu + a.GL - 1) / a.GL <= persist::UPP &&
-           (a.D + a.GL - 1) / a.GL <= persist::UPP && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
+           (a.D + a.GL - 1) / a.GL <= persist::UPP && a.D / 4 <= persist::NT && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
            a.n_layers >= 1 && a.GL >= 1 && a.GL < 256 && (!a.xcd || a.GL == 32);
 }
 
