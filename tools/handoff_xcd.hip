@@ -30,16 +30,18 @@ typedef unsigned long long u64;
 // MODE 2: workgroup-scope store + L1 invalidate (buffer_inv sc0) + plain load per poll round
 // MODE 3: workgroup-scope store + agent-scope load
 // MODE 4: agent-scope store + L1 invalidate + plain load
+// MODE 5: non-temporal store (nt) + agent-scope load
 template <int MODE>
 __device__ __forceinline__ void put(u64* g, unsigned tag, float v) {
     const u64 x = ((u64)tag << 32) | __float_as_uint(v);
     if (MODE == 0 || MODE == 4) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (MODE == 5) __builtin_nontemporal_store(x, g);
     else __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 template <int MODE>
 __device__ __forceinline__ u64 get(u64* base, __amdgpu_buffer_rsrc_t r, int idx) {
-    if (MODE == 0 || MODE == 3) return __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (MODE == 0 || MODE == 3 || MODE == 5) return __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (MODE == 2 || MODE == 4) return __hip_atomic_load(base + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, idx * 8, 0, 1);  // sc0: miss L1
     return (u64)(unsigned)v[0] | ((u64)(unsigned)v[1] << 32);
@@ -121,7 +123,8 @@ int main() {
     CK(hipEventCreate(&e1));
     struct Cfg { int mode, stride; const char* name; } cfgs[] = {
         {0, 1, "agent, all 256 wgs"}, {0, 8, "agent, wg%8==0 (32)"}, {2, 8, "wg st, inv+ld (32)"},
-        {3, 8, "wg st, agent ld (32)"}, {4, 8, "agent st, inv+ld (32)"}, {1, 8, "wg st, sc0 ld (32)"}};
+        {3, 8, "wg st, agent ld (32)"}, {4, 8, "agent st, inv+ld (32)"}, {1, 8, "wg st, sc0 ld (32)"},
+        {5, 1, "nt st, agent ld, all 256"}, {5, 4, "nt st, agent ld (64)"}, {0, 4, "agent, wg%4==0 (64)"}};
     for (const Cfg& cf : cfgs)
         for (int V : Vs) {
             double us[2];
@@ -131,7 +134,7 @@ int main() {
                     CK(hipMemsetAsync(buf, 0, (size_t)E * V * 8, s));
                     switch (cf.mode) {
 #define CASE(M) case M: hipLaunchKernelGGL((chain_kernel<4, M>), dim3(grid), dim3(256), 0, s, buf, edges, V, cf.stride, out, tmo, xcc); break;
-                        CASE(0) CASE(1) CASE(2) CASE(3) CASE(4)
+                        CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5)
 #undef CASE
                     }
                 };
