@@ -715,7 +715,7 @@ __global__ void xcc_probe_kernel(unsigned* out) {
     if (threadIdx.x == 0) out[blockIdx.x] = persist::xcc_id();
 }
 
-int decode_persist_xcd_probe(unsigned* xcc) {
+int decode_persist_xcd_probe() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 256)
@@ -730,7 +730,6 @@ int decode_persist_xcd_probe(unsigned* xcc) {
         for (int i = 0; i < 256 && ok; ++i) ok = (i % 8 == 0) == (h[i] == h[0]);
     }
     (void)hipFree(d);
-    if (ok) *xcc = h[0];
     return ok ? 1 : 0;
 }
 

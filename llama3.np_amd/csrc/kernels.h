@@ -244,7 +244,6 @@ struct DecodePersistArgs {
     int GL;                        // workgroups that run the layer stages (the others: the lm_head)
     int xcd;                       // 1: the layer stages on one XCD (GL = 32, wg % 8 == 0), XCD-local
                                    //    hand-offs; 0: GL = 64 workgroups over all XCDs
-    unsigned xcc;                  // xcd: the XCD id the layer workgroups must find (checked)
     int Dp, Xp;                    // LDS floats: per D-vector, per stage-input vector (multiples of 4)
     float eps, q_scale;
     const float* emb;              // [VS, D]
@@ -274,7 +273,7 @@ __host__ __device__ inline int64_t decode_persist_slab(int H, int KVH, int HD, i
 }
 bool decode_persist_ok(const DecodePersistArgs& a);
 hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s);
-int decode_persist_xcd_probe(unsigned* xcc);  // 1: wg % 8 == 0 share one XCD (its id in *xcc)
+int decode_persist_xcd_probe();  // 1: the workgroups wg % 8 == 0 of a grid share one XCD
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);

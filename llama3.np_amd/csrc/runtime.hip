@@ -212,7 +212,6 @@ struct l3_ctx {
     bool persist_ready = false;
     bool persist_graph = false;      // the captured single-step graph runs the persistent step
     int persist_xcd_ok = -1;         // wg % 8 == 0 on one XCD (decode_persist_xcd_probe); -1: not probed
-    unsigned persist_xcc = 0;
     bool persist_xcd = false;        // this capture: the one-XCD layout (L3_DECODE_PERSIST=2)
 };
 
@@ -963,7 +962,7 @@ static bool persist_wanted(l3_ctx* c, int B) {
     // read at every capture (captures are rare), so a process can A/B the paths
     const int mode = env_knob("L3_DECODE_PERSIST", 1);
     if (!mode || B != 1 || c->layers.empty() || !c->dec_state) return false;
-    if (mode == 2 && c->persist_xcd_ok < 0) c->persist_xcd_ok = decode_persist_xcd_probe(&c->persist_xcc);
+    if (mode == 2 && c->persist_xcd_ok < 0) c->persist_xcd_ok = decode_persist_xcd_probe();
     DecodePersistArgs a{};
     a.D = c->d.dim; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads; a.HD = c->HD; a.FD = c->d.hidden_dim;
     a.VS = c->d.vocab_size; a.n_layers = (int)c->layers.size(); a.Smax = c->d.max_seq_len;
@@ -1067,7 +1066,6 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
         a.kv_bak = c->bak_capture ? c->kv_bak : nullptr;
         a.xcd = c->persist_xcd ? 1 : 0;
         a.GL = a.xcd ? 32 : 64;
-        a.xcc = c->persist_xcc;
         a.from_parts = i > 0;            // the previous step in this graph left partials only
         a.write_id = i == steps - 1;     // the last one publishes the id for the host / next graph
         const hipError_t e = launch_decode_persist(a, c->stream);
