@@ -24,6 +24,7 @@
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <chrono>
 #include <deque>
@@ -211,6 +212,8 @@ struct l3_ctx {
     DecodePersistArgs persist{};
     bool persist_ready = false;
     bool persist_graph = false;      // the captured single-step graph runs the persistent step
+    hipEvent_t order_ev = nullptr;   // after this context's last decode graph (launch_decode_graph)
+    bool order_registered = false;
     int persist_xcd_ok = -1;         // wg % 8 == 0 on one XCD (decode_persist_xcd_probe); -1: not probed
     bool persist_xcd = false;        // this capture: the one-XCD layout (L3_DECODE_PERSIST=2)
 };
@@ -343,6 +346,35 @@ extern "C" int l3_device_count(int32_t* n) {
     return 0;
 }
 
+// Persistent decode steps need every CU of their device at once (decode_persist.hip): two running
+// together — decode graphs of two contexts on one device, e.g. two models' lazy generators
+// interleaved, each queued steps ahead — would each hold part of the CUs and wait for the rest
+// until their bounded spins fail.  So while a device has several contexts, their decode graphs
+// are ordered: each waits for the last one another context queued.
+namespace {
+struct DevOrder {
+    std::mutex m;
+    int contexts = 0;
+    const l3_ctx* owner = nullptr;  // the context that queued the last decode graph
+    hipEvent_t ev = nullptr;        // its order_ev, recorded after that graph
+};
+DevOrder g_order[64];
+}  // namespace
+
+static int launch_decode_graph(l3_ctx* c, hipGraphExec_t g) {
+    DevOrder& d = g_order[c->device & 63];
+    std::lock_guard<std::mutex> lk(d.m);
+    if (d.contexts > 1 && d.ev && d.owner != c) HIP_TRY(hipStreamWaitEvent(c->stream, d.ev, 0));
+    HIP_TRY(hipGraphLaunch(g, c->stream));
+    if (d.contexts > 1) {
+        if (!c->order_ev) HIP_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->order_ev, c->stream));
+        d.ev = c->order_ev;
+        d.owner = c;
+    }
+    return 0;
+}
+
 extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     if (!dims || !out) return fail("l3_create: null argument");
     const l3_dims& d = *dims;
@@ -371,6 +403,12 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     c->qkvn = c->qdim + 2 * c->kvdim;
     auto bail = [&](int rc) { l3_destroy(c); return rc; };
     if (set_dev(c)) return bail(1);
+    {
+        DevOrder& o = g_order[device & 63];
+        std::lock_guard<std::mutex> lk(o.m);
+        ++o.contexts;
+        c->order_registered = true;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
         return bail(fail("hipStreamCreate / hipEventCreate failed"));
@@ -440,6 +478,13 @@ extern "C" int l3_destroy(l3_ctx* c) {
     for (auto& q : c->spec_q) { (void)hipEventDestroy(q.ev0); (void)hipEventDestroy(q.ev1); (void)hipEventDestroy(q.ev); }
     for (hipEvent_t e : c->spec_free) (void)hipEventDestroy(e);
     dfree(c->spec_hist);
+    if (c->order_registered) {
+        DevOrder& o = g_order[c->device & 63];
+        std::lock_guard<std::mutex> lk(o.m);
+        --o.contexts;
+        if (o.owner == c) { o.owner = nullptr; o.ev = nullptr; }
+    }
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     dfree(c->persist_mem);
     dfree(c->persist.stamps);
     if (c->persist_err) (void)hipHostFree(c->persist_err);
@@ -1233,7 +1278,7 @@ static int speculate(l3_ctx* c, int B) {
             }
         }
         HIP_TRY(hipEventRecord(ev[0], c->stream));
-        HIP_TRY(hipGraphLaunch(k > 1 ? c->dec_exec_n : c->dec_exec, c->stream));
+        if (launch_decode_graph(c, k > 1 ? c->dec_exec_n : c->dec_exec)) return 1;
         HIP_TRY(hipEventRecord(ev[1], c->stream));
         HIP_TRY(hipMemcpyAsync(c->spec_ids + (size_t)c->spec_end * B, c->spec_hist + (size_t)c->spec_end * B,
                                (size_t)k * B * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1314,7 +1359,7 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
     for (int i = 0; replay && i < B; ++i) replay = c->dec_last[(size_t)i] == ids_host[i];
     if (replay) {
         const double t0 = now_us();
-        HIP_TRY(hipGraphLaunch(c->dec_exec, c->stream));
+        if (launch_decode_graph(c, c->dec_exec)) return 1;
         HIP_TRY(hipMemcpyAsync(c->dec_host, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         if (persist_check(c)) return 1;
@@ -1421,8 +1466,7 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
     if (n > 1 && steps - 2 >= n && ensure_multi_graph(c, B)) return done(1);
     for (int i = 2; i < steps;) {
         const bool multi = n > 1 && steps - i >= n;
-        if (hipGraphLaunch(multi ? c->dec_exec_n : c->dec_exec, c->stream) != hipSuccess)
-            return done(fail("generate: graph replay failed"));
+        if (launch_decode_graph(c, multi ? c->dec_exec_n : c->dec_exec)) return done(1);
         i += multi ? n : 1;
         c->graph_steps += multi ? n : 1;
     }

@@ -1134,6 +1134,28 @@ def test_c5_full_depth_full_size_rows_match_b1():
     print(f"c5 32 layers B=64 L=2048: rows vs B=1 max-abs {errs}, |logits| <= {float(np.abs(out).max()):.2f}")
 
 
+def test_persistent_decode_two_contexts_one_device(tmpdir_mod):
+    """Two models on one GPU, their lazy generators interleaved token by token (each queues
+    persistent decode steps ahead of its caller): a persistent step needs every CU at once, so the
+    two contexts' decode graphs are ordered on the device (runtime.hip launch_decode_graph) — both
+    streams of ids equal the reference's 145 greedy ids (llama3.py:310-321), no hand-off times out."""
+    g = load_golden("stories15m_default")
+    args = synth.stories15m(1)
+    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, int(g["seed"]), "default")
+    prompt = np.asarray(g["dream_prompt"]).reshape(1, -1)
+    want = np.asarray(g["dream_ids"]).reshape(1, -1)
+    n = int(g["dream_max_new"])
+    a, b = llama3.Llama(path, args), llama3.Llama(path, args)
+    ga, gb = a.generate(prompt, n), b.generate(prompt, n)
+    got_a, got_b = [], []
+    for x, y in zip(ga, gb):  # one token from each in turn (the generators stop where the reference's does)
+        got_a.append(x)
+        got_b.append(y)
+    np.testing.assert_array_equal(np.concatenate(got_a, axis=1), want)
+    np.testing.assert_array_equal(np.concatenate(got_b, axis=1), want)
+    assert a.context.decode_persistent() and b.context.decode_persistent()
+
+
 @pytest.mark.parametrize("preset", ["default", "sharp"])
 def test_persistent_decode_step_matches_golden(tmpdir_mod, monkeypatch, preset):
     """The persistent batch-1 decode step (decode_persist.hip: one launch per greedy step, every
