@@ -10,7 +10,10 @@
 // step averages 3.8 us per kernel).  Inside one launch an all-to-all hand-off measured 1.85-2.3
 // us (tools/handoff_chain, profiles/r04_handoff_chain.log), about a boundary — so the gain must
 // come from what a boundary forbids: every workgroup issues the NEXT stage's weight loads right
-// after publishing the current stage, and they land while it waits for the hand-off.
+// after publishing the current stage, and they land while it waits for the hand-off.  Measured:
+// 0.076 ms per greedy step in the device loop against 0.096-0.098 for the 25-kernel graph
+// (profiles/r04_persist_decode_ab.log); the stages are VALU-bound at one wave per SIMD, so every
+// select, branch and workgroup reduction on the critical path shows (DESIGN.md decisions table).
 //
 // Hand-offs (cdna_hip_programming.md Guideline 16, R2): every stage output value travels as one
 // 8-byte {tag, value} granule written by ONE agent-scope relaxed atomic store (sc1 write-through);
