@@ -1134,7 +1134,7 @@ def test_c5_full_depth_full_size_rows_match_b1():
     print(f"c5 32 layers B=64 L=2048: rows vs B=1 max-abs {errs}, |logits| <= {float(np.abs(out).max()):.2f}")
 
 
-def test_persistent_decode_two_contexts_one_device(tmpdir_mod):
+def test_persistent_decode_two_contexts_one_device(tmpdir_mod, monkeypatch):
     """Two models on one GPU, their lazy generators interleaved token by token (each queues
     persistent decode steps ahead of its caller): a persistent step needs every CU at once, so the
     two contexts' decode graphs are ordered on the device (runtime.hip launch_decode_graph) — both
@@ -1145,6 +1145,7 @@ def test_persistent_decode_two_contexts_one_device(tmpdir_mod):
     prompt = np.asarray(g["dream_prompt"]).reshape(1, -1)
     want = np.asarray(g["dream_ids"]).reshape(1, -1)
     n = int(g["dream_max_new"])
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
     a, b = llama3.Llama(path, args), llama3.Llama(path, args)
     ga, gb = a.generate(prompt, n), b.generate(prompt, n)
     got_a, got_b = [], []
