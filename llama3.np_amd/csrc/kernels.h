@@ -166,9 +166,10 @@ __device__ __forceinline__ float group_max(float v) {
 // np.argmax order (llama3.py:320): larger value first, ties to the lower index, a NaN beats any
 // number and the first NaN wins (a strict total order, so any reduction tree gives the same id)
 __device__ __forceinline__ bool argmax_better(float v, int i, float bv, int bi) {
-    const bool vn = v != v, bn = bv != bv;
-    if (vn || bn) return vn && (!bn || i < bi);
-    return v > bv || (v == bv && i < bi);
+    const bool vn = v != v, bn = bv != bv, lo = i < bi;
+    // one boolean expression (selects, no branches): the same order as
+    //   vn || bn ? vn && (!bn || lo) : v > bv || (v == bv && lo)
+    return (vn & (!bn | lo)) | (!vn & !bn & ((v > bv) | ((v == bv) & lo)));
 }
 
 // (value, index) argmax over aligned groups of LANES lanes on the VALU (the group_sum pattern of
@@ -181,7 +182,9 @@ __device__ __forceinline__ int dpp_mov_i(int v) {
 template <int LANES>
 __device__ __forceinline__ void group_argmax(float& best, int& bi, int lane) {
     auto step = [&](float ov, int oi) {
-        if (argmax_better(ov, oi, best, bi)) { best = ov; bi = oi; }
+        const bool t = argmax_better(ov, oi, best, bi);
+        best = t ? ov : best;
+        bi = t ? oi : bi;
     };
     step(__int_as_float(dpp_mov_i<0xB1>(__float_as_int(best))), dpp_mov_i<0xB1>(bi));
     step(__int_as_float(dpp_mov_i<0x4E>(__float_as_int(best))), dpp_mov_i<0x4E>(bi));
