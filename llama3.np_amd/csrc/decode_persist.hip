@@ -519,19 +519,21 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
             const int S = pos + 1;
             // key tid from the prefetched row (rows past HD are zero: the q4 reads past HD land
-            // in the k / v part of qs and add nothing); the new key (tid == pos) from k_new, in
-            // the same unrolled pass — a lane of its own looping over LDS held its whole wave
-            // (and the block_max barrier) back ~0.7 us
-            if (tid == pos) {
-#pragma unroll
-                for (int i = 0; i < KPF; ++i) kr[i] = i < D4 ? kn4[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-            }
+            // in the k / v part of qs and add nothing).  The new key's score (key pos, from k_new)
+            // is computed by every 16-lane group at once — chunk j of q . k_new, summed over the
+            // group — and selected by lane pos: loading k_new into that one lane's row was a
+            // divergent branch that held its wave (and the block_max barrier) back ~0.3 us
+            const int jn = min(tid & 15, D4 - 1);
+            const f32x4 qn = q4[jn], kn = kn4[jn];
+            float s_new = (tid & 15) < D4 ? qn.x * kn.x + qn.y * kn.y + qn.z * kn.z + qn.w * kn.w : 0.f;
+            s_new = group_sum<16>(s_new);
             float s_own = 0.f;
 #pragma unroll
             for (int i = 0; i < KPF; ++i) {
                 const f32x4 b = q4[i];
                 s_own += kr[i].x * b.x + kr[i].y * b.y + kr[i].z * b.z + kr[i].w * b.w;
             }
+            s_own = tid == pos ? s_new : s_own;
             float m = -INFINITY;
             if (tid < S) {
                 sc[tid] = s_own;
