@@ -571,7 +571,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
 #pragma unroll
                 for (int t = 0; t < VPF; ++t) acc += (rg + t * R < pos ? pk[t] : 0.f) * vr[t];
                 for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
-                if (pos % R == rg) acc += sc[pos] * vn4[d4];
+                // the new key's row: every lane reads it, the key group owning it adds it (no
+                // divergent reads before the partials' barrier)
+                const float pn = sc[pos];
+                const f32x4 vn = vn4[d4];
+                acc += (pos % R == rg ? pn : 0.f) * vn;
             }
             if (li == 1) stamp(113);
             f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
