@@ -213,7 +213,6 @@ struct l3_ctx {
     bool persist_ready = false;
     bool persist_graph = false;      // the captured single-step graph runs the persistent step
     hipEvent_t order_ev = nullptr;   // after this context's last decode graph (launch_decode_graph)
-    bool order_registered = false;
     int persist_xcd_ok = -1;         // wg % 8 == 0 on one XCD (decode_persist_xcd_probe); -1: not probed
     bool persist_xcd = false;        // this capture: the one-XCD layout (L3_DECODE_PERSIST=2)
 };
@@ -349,12 +348,11 @@ extern "C" int l3_device_count(int32_t* n) {
 // Persistent decode steps need every CU of their device at once (decode_persist.hip): two running
 // together — decode graphs of two contexts on one device, e.g. two models' lazy generators
 // interleaved, each queued steps ahead — would each hold part of the CUs and wait for the rest
-// until their bounded spins fail.  So while a device has several contexts, their decode graphs
-// are ordered: each waits for the last one another context queued.
+// until their bounded spins fail.  So the decode graphs of a device's contexts are ordered: each
+// waits for the last one another context queued.
 namespace {
 struct DevOrder {
     std::mutex m;
-    int contexts = 0;
     const l3_ctx* owner = nullptr;  // the context that queued the last decode graph
     hipEvent_t ev = nullptr;        // its order_ev, recorded after that graph
 };
@@ -364,14 +362,14 @@ DevOrder g_order[64];
 static int launch_decode_graph(l3_ctx* c, hipGraphExec_t g) {
     DevOrder& d = g_order[c->device & 63];
     std::lock_guard<std::mutex> lk(d.m);
-    if (d.contexts > 1 && d.ev && d.owner != c) HIP_TRY(hipStreamWaitEvent(c->stream, d.ev, 0));
+    if (d.ev && d.owner != c) HIP_TRY(hipStreamWaitEvent(c->stream, d.ev, 0));
     HIP_TRY(hipGraphLaunch(g, c->stream));
-    if (d.contexts > 1) {
-        if (!c->order_ev) HIP_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(c->order_ev, c->stream));
-        d.ev = c->order_ev;
-        d.owner = c;
-    }
+    // recorded even while this is the device's only context: one created later must still wait
+    // for the graphs this one has already queued (run-ahead)
+    if (!c->order_ev) HIP_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->order_ev, c->stream));
+    d.ev = c->order_ev;
+    d.owner = c;
     return 0;
 }
 
@@ -403,12 +401,6 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     c->qkvn = c->qdim + 2 * c->kvdim;
     auto bail = [&](int rc) { l3_destroy(c); return rc; };
     if (set_dev(c)) return bail(1);
-    {
-        DevOrder& o = g_order[device & 63];
-        std::lock_guard<std::mutex> lk(o.m);
-        ++o.contexts;
-        c->order_registered = true;
-    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
         return bail(fail("hipStreamCreate / hipEventCreate failed"));
@@ -478,10 +470,9 @@ extern "C" int l3_destroy(l3_ctx* c) {
     for (auto& q : c->spec_q) { (void)hipEventDestroy(q.ev0); (void)hipEventDestroy(q.ev1); (void)hipEventDestroy(q.ev); }
     for (hipEvent_t e : c->spec_free) (void)hipEventDestroy(e);
     dfree(c->spec_hist);
-    if (c->order_registered) {
+    {
         DevOrder& o = g_order[c->device & 63];
         std::lock_guard<std::mutex> lk(o.m);
-        --o.contexts;
         if (o.owner == c) { o.owner = nullptr; o.ev = nullptr; }
     }
     if (c->order_ev) (void)hipEventDestroy(c->order_ev);
