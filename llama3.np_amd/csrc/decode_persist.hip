@@ -434,11 +434,14 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         // launches), fetched in stage B before its hand-off wait (fetched at the layer's start
         // instead, ahead of the QKV rows, the step measured 0.091 against 0.087 ms)
         const int kvh = lw / (H / KVH);
-        const int D4 = HD / 4, R = NT / D4;  // PV: R key groups x D4 float4 columns
-        const int rg = tid / D4, d4 = tid - rg * D4;
+        // P.V layout: 16 key groups (rg, one 16-lane row each) x 16 float4 columns (d4; the ones
+        // past HD / 4 idle), so a wave's four key groups reduce across its rows on the VALU
+        const int D4 = HD / 4;
+        constexpr int R = NT / 16;
+        const int rg = tid >> 4, d4 = min(tid & 15, D4 - 1);
         const f32x4* K4p = reinterpret_cast<const f32x4*>(ck + (int64_t)kvh * p.Smax * HD);
         const f32x4* V4p = reinterpret_cast<const f32x4*>(cv + (int64_t)kvh * p.Smax * HD);
-        constexpr int VPF = (NT + NT / KPF - 1) / (NT / KPF);  // V rows per lane: the first NT keys
+        constexpr int VPF = NT / R;  // V rows per lane: the first NT keys
         // unpredicated loads from clamped rows (see load_rows), zeroed where used; row pos - 1 is
         // the last one an earlier launch wrote (pos >= 1 in a decode step)
         const int kmax = pos > 0 ? pos - 1 : 0;
@@ -502,7 +505,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
 #pragma unroll
             for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
 #pragma unroll
-            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + min(d4, D4 - 1)];
+            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + d4];
             if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
                 goto done;
             stamp(3 + 10 * li);
@@ -562,7 +565,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             l = block_sum(c, l);  // its barrier also publishes sc
             if (li == 1) stamp(112);
             f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            if (rg < R) {
+            {
                 // every p read first (clamped index), then the FMAs with p zeroed past pos: a
                 // predicated read per key was a branch and an LDS wait per key
                 float pk[VPF];
@@ -578,21 +581,24 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 acc += (pos % R == rg ? pn : 0.f) * vn;
             }
             if (li == 1) stamp(113);
+            // the four key groups of a wave summed across its 16-lane rows (permlane swaps), then
+            // the four waves' sums through LDS (a chain of 21 dependent adds over LDS partials
+            // was ~0.4 us)
+            {
+                auto rows = [](float v) {
+                    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+                    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+                };
+                acc = f32x4{rows(acc.x), rows(acc.y), rows(acc.z), rows(acc.w)};
+            }
             f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
-            if (rg < R) part[rg * D4 + d4] = acc;
+            if ((tid & 63) < 16) part[(tid >> 6) * 16 + (tid & 15)] = acc;
             lds_barrier();
             if (li == 1) stamp(114);
             if (tid < D4) {
-                // the first NT / KPF key groups' partials read in one go (R >= that: D4 <= KPF),
-                // then added in order (a loop of read-wait-add was ~0.9 us of LDS round trips)
-                constexpr int RC = NT / KPF;
-                f32x4 pr[RC];
-#pragma unroll
-                for (int r = 0; r < RC; ++r) pr[r] = part[r * D4 + tid];
-                f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int r = 0; r < RC; ++r) o += pr[r];
-                for (int r = RC; r < R; ++r) o += part[r * D4 + tid];
+                f32x4 o = (part[tid] + part[16 + tid]) + (part[32 + tid] + part[48 + tid]);
                 o *= 1.0f / l;
                 gput_s<XL>(g_o + qo + 4 * tid + 0, tag, o.x);
                 gput_s<XL>(g_o + qo + 4 * tid + 1, tag, o.y);
