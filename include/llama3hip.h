@@ -138,6 +138,12 @@ int l3_greedy_step_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t
  * hipGraph replay, one copy-back at the end).  out_ids_host [B, max_new_tokens - L]. */
 int l3_greedy_generate_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
                             int32_t max_new_tokens, int64_t* out_ids_host);
+/* The same loop, also returning each step's winning logit (the value np.argmax picked at
+ * llama3.py:320, i.e. logits[b, -1, id]) in out_vals [B, max_new_tokens - L] fp32: the replayed
+ * steps record it beside the id on the device, the eager steps read it from their logits rows.
+ * Pins a decode path's values, not only its ids, against the reference (extension). */
+int l3_greedy_generate_values_host(l3_ctx* ctx, const int64_t* ids_host, int32_t B, int32_t L,
+                                   int32_t max_new_tokens, int64_t* out_ids_host, float* out_vals);
 
 /* ---- one block (replaces TransformerBlock.__call__, llama3.py:239-261) --- */
 /* x [B, L, D] fp32 host -> out [B, L, D]; uses and updates layer's KV cache. */
@@ -201,9 +207,14 @@ int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits
 /* Whether the captured batch-1 decode step is the persistent kernel (one launch per greedy step,
  * decode_persist.hip: every layer, the lm_head and the argmax with in-launch hand-offs) rather
  * than the 25-kernel graph.  The persistent step is the default for shapes it takes (HD <= 64,
- * decode_persist_ok); env L3_DECODE_PERSIST (read at capture): 1 default, 2 layer stages on one
- * XCD, 0 the graph. */
+ * decode_persist_ok) on devices it can run on (every one of its workgroups resident: enough CUs,
+ * checked at capture; otherwise the graph is captured); env L3_DECODE_PERSIST (read at capture):
+ * 1 default, 0 the graph.  A persistent step that gives up on an in-launch hand-off is recovered,
+ * not reported: the steps queued ahead are undone, the step runs again on the graph path with
+ * the same result, and the context stays on the graph path (l3_decode_recoveries counts this). */
 int l3_decode_persistent(l3_ctx* ctx, int32_t* active);
+/* Persistent decode steps recovered on the graph path over the context's life (see above). */
+int l3_decode_recoveries(l3_ctx* ctx, int64_t* count);
 /* Lazy greedy decode runs up to 16 steps ahead of the caller on the device (undone if the
  * caller leaves the schedule, so results are unchanged), and at most ~4 ms of decode work by
  * the measured step time: a caller that stops early (EOS, an abandoned generator) or makes any

@@ -20,19 +20,28 @@
 // consumers re-read the granules they need with agent-scope relaxed loads (sc1, L1-bypassing)
 // until every tag equals the launch's epoch.  Each (layer, stage) has its own granule slab, so no
 // slab is rewritten inside a launch; the epoch (a device word, +1 at the end of every launch by
-// workgroup 0, after every other workgroup has published its last value) makes the previous
-// launch's granules stale without a memset.  Only values produced in THIS launch travel as
-// granules; everything older (weights, the KV rows of earlier positions, the token id) is read
-// with plain loads, which a kernel boundary makes visible.  Spins are bounded: a workgroup that
-// waits ~1 s sets the error word (host-mapped) and leaves, so a fault ends the launch instead of
-// hanging it; the host checks the word after every synchronised step.
+// workgroup 0, once every workgroup of the launch has published its start mark, i.e. has read the
+// launch's tag) makes the previous launch's granules stale without a memset.  Only values produced
+// in THIS launch travel as granules; everything older (weights, the KV rows of earlier positions,
+// the token id) is read with plain loads, which a kernel boundary makes visible.
 //
-// Work split (grid = 256 workgroups x 256 threads, all resident: 1 per CU by resources): the layer
-// stages run on workgroups 0..GL-1 (GL = 64, eight per XCD under round-robin dispatch); the
-// attention of head h on workgroup h; the lm_head's 32000 rows on all 256 (workgroups >= GL load
-// their rows while the layers run).  GEMV stages: 16 lanes per output unit (a row, or a RoPE /
-// gate-up row pair), the unit's W rows in registers, the input vector staged once per workgroup
-// in LDS.
+// Failure is all-or-nothing for the KV caches.  Spins are bounded: a workgroup that waits ~1 s
+// (the layer chain), or that finds the sticky failure word another workgroup set (the lm_head
+// and the final argmax), gives up — it sets that word and the host-mapped error word (the step's
+// position + 1) and leaves — so a fault ends the launch instead of hanging it, and every later
+// launch returns at once until the host has recovered (runtime.hip persist_recover: undo, then
+// the 25-kernel graph path).  A layer workgroup keeps the K / V rows its stage A computes (and,
+// for the run-ahead undo, the slots' previous contents) in LDS and writes them to the caches only
+// after its last wait of the step, which every layer workgroup passes exactly when every stage of
+// every layer has published; workgroup 0 records that point (epoch[2] = pos + 1), so after a
+// failure the host knows whether the step's slots were written (all of them) or not (none).
+//
+// Work split (grid = 256 workgroups x 256 threads, all resident: 1 per CU by resources, checked
+// against the device by decode_persist_grid before a capture): the layer stages run on workgroups
+// 0..GL-1 (GL = 64); the attention of head h on workgroup h; the lm_head's 32000 rows on the
+// workgroups >= GL (they load their rows while the layers run).  GEMV stages: 16 lanes per output
+// unit (a row, or a RoPE / gate-up row pair), the unit's W rows in registers, the input vector
+// staged once per workgroup in LDS.
 #include "kernels.h"
 
 namespace l3 {
@@ -52,24 +61,6 @@ __device__ __forceinline__ void gput(u64* g, unsigned tag, float v) {
 __device__ __forceinline__ u64 gget(u64* g) {
     return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// XCD-local hand-offs (DecodePersistArgs::xcd: every producer and consumer on one XCD, sharing its
-// L2): the granule store stops at that L2 (workgroup scope: no sc1 write-through to memory) and the
-// consumers' agent-scope loads find it there.  tools/handoff_xcd, 32 workgroups on one XCD: 1.0 us
-// per all-to-all edge against 1.73 with the write-through store (2.63 over all 8 XCDs); the
-// load forms that stop at the L1 or L2 of their own (sc0, L1 invalidate + plain load) never saw
-// the stores and timed out.  Only for consumers on the producer's XCD.
-__device__ __forceinline__ void gput_xcd(u64* g, unsigned tag, float v) {
-    __hip_atomic_store(g, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-template <bool LOCAL>
-__device__ __forceinline__ void gput_s(u64* g, unsigned tag, float v) {
-    if (LOCAL) gput_xcd(g, tag, v);
-    else gput(g, tag, v);
-}
-__device__ __forceinline__ unsigned xcc_id() {  // HW_REG_XCC_ID (hwreg 20), bits [3:0]
-    return __builtin_amdgcn_s_getreg((20) | (0 << 6) | ((16 - 1) << 11)) & 0xf;
-}
-
 // Workgroup barrier for LDS traffic only: __syncthreads() is also a workgroup-scope release of
 // global memory, i.e. an s_waitcnt vmcnt(0) that waits for this wave's write-through granule /
 // cache / stamp stores to be acknowledged (~1 us) before the barrier.  Nothing in this kernel
@@ -88,17 +79,25 @@ struct Ctx {
     float* red;         // LDS scratch [NT]
 };
 
+// the step's position + 1 to the host-mapped error word; epoch[1] sticky (every workgroup still
+// waiting gives up at its next check, every later launch returns at once)
 __device__ __forceinline__ void give_up(const Ctx& c) {
     *c.bad = 1;
-    __hip_atomic_store(c.p.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(c.p.epoch + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sticky
+    __hip_atomic_store(c.p.err, (unsigned)c.pos + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(c.p.epoch + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool sticky(const Ctx& c) {
+    return __hip_atomic_load(c.p.epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
 }
 
-// granules g[idx(i)] for i < n into dst[i] (LDS), every thread its i = tid + NT*k, all of a
-// thread's loads in flight per pass; re-read until every tag is the launch's.  Ends with a
-// workgroup barrier; false if this workgroup gave up (caller returns).
+// granules g[idx(i)] for i < n, the first nst of them into dst[i] (LDS; the rest only waited
+// for), every thread its i = tid + NT*k, all of a thread's loads in flight per pass; re-read until
+// every tag is the launch's.  Ends with a workgroup barrier; false if this workgroup gave up
+// (caller returns).  stick: also give up once another workgroup has (the sticky word) — not in
+// the layer chain, whose workgroups wait the full bound instead, so that the chain either
+// completes for every layer workgroup or for none (the K / V write, see the header)
 template <int PER, typename Idx>
-__device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
+__device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep, bool stick, int nst) {
     const int tid = threadIdx.x;
     bool ok = false;
     for (unsigned spin = 0;; ++spin) {
@@ -113,11 +112,12 @@ __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, I
 #pragma unroll
             for (int k = 0; k < PER; ++k) {
                 const int i = tid + NT * k;
-                if (i < n) dst[i] = __uint_as_float((unsigned)x[k]);
+                if (i < nst) dst[i] = __uint_as_float((unsigned)x[k]);
             }
             break;
         }
-        if (spin > (1u << 20) || ((spin & 255) == 255 && *c.bad)) {  // another wave gave up
+        // ~1 s, or another wave of this workgroup / (stick) another workgroup gave up
+        if (spin > (1u << 20) || ((spin & 255) == 255 && (*c.bad || (stick && sticky(c))))) {
             give_up(c);
             break;
         }
@@ -129,10 +129,13 @@ __device__ __forceinline__ bool sweep(const Ctx& c, u64* g, int n, float* dst, I
 }
 
 template <typename Idx>
-__device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1) {
-    if (n <= NT) return sweep<1>(c, g, n, dst, idx, sleep);
-    if (n <= 2 * NT) return sweep<2>(c, g, n, dst, idx, sleep);
-    return sweep<4>(c, g, n, dst, idx, sleep);  // n <= 1024 (eligibility)
+__device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst, Idx idx, int sleep = 1,
+                                        bool stick = false, int nst = -1) {
+    if (nst < 0) nst = n;
+    if (n <= NT) return sweep<1>(c, g, n, dst, idx, sleep, stick, nst);
+    if (n <= 2 * NT) return sweep<2>(c, g, n, dst, idx, sleep, stick, nst);
+    if (n <= 4 * NT) return sweep<4>(c, g, n, dst, idx, sleep, stick, nst);
+    return sweep<5>(c, g, n, dst, idx, sleep, stick, nst);  // n <= 1280: FD (<= 1024) + the start marks
 }
 
 // block max / sum of one value per thread (every thread gets it), one barrier each: the two use
@@ -254,12 +257,11 @@ __device__ __forceinline__ int stage_unit(const DecodePersistArgs& p, int n, int
 }  // namespace persist
 
 // One launch = one decode step.  Granule slab per layer: [qkv | o | h1 | hid | h2]
-// (decode_persist_slab), then the lm_head partials [2 * gridDim.x].
-// NCD / NCF: float4 per lane of a W row with K = D / K = FD (>= ceil(K / 64)); KPF >= HD / 4; LMPF:
-// lm_head passes of 16 rows each workgroup holds in registers.  XL: the layer stages on the 32
-// workgroups of one XCD (wg % 8 == 0; DecodePersistArgs::xcd) with XCD-local hand-offs, two hidden
-// units per gate|up unit; only the last layer's output and the lm partials cross XCDs
-template <int NCD, int NCF, int KPF, int LMPF, bool XL>
+// (decode_persist_slab), then the lm_head partials [2 * 256], then the start marks [256].
+// NCD / NCF: float4 per lane of a W row with K = D / K = FD (>= ceil(K / 64)); KPF >= HD / 4 (the
+// old keys' chunks each attention lane holds); LMPF: lm_head passes of 16 rows each workgroup
+// holds in registers.
+template <int NCD, int NCF, int KPF, int LMPF>
 __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArgs p) {
     using namespace persist;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -267,7 +269,8 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     __shared__ float red_s[NT];
     const int D = p.D, HD = p.HD, H = p.H, KVH = p.KVH, FD = p.FD;
     const int qdim = H * HD, kvdim = KVH * HD, qkvn = qdim + 2 * kvdim;
-    float* hin = sm;              // [D]  layer input (residual of the O-proj)
+    f32x4* kvs = reinterpret_cast<f32x4*>(sm);  // [n_layers][UPP] this workgroup's K / V pairs: new, old
+    float* hin = sm + 4 * UPP * p.n_layers;     // [D]  layer input (residual of the O-proj)
     float* h1s = hin + p.Dp;      // [D]  FFN input (residual of the down-proj)
     float* xs = h1s + p.Dp;       // [max(qkvn, FD, qdim)] stage input
     float* sc = xs + p.Xp;        // [Smax] attention scores
@@ -276,32 +279,40 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     const unsigned tag = p.epoch[0];
     const int pos = p.st->pos;
     int id = p.ids[0];
-    // an earlier launch gave up (epoch[1], sticky): do nothing, the host reports it
+    // an earlier launch gave up (epoch[1], sticky): do nothing, the host recovers
     if (p.epoch[1]) return;
+    const int64_t slab = decode_persist_slab(H, KVH, HD, D, FD);
+    u64* lm_g = p.gran + slab * p.n_layers;
+    u64* marks = lm_g + 2 * 256;
+    // start mark: this workgroup has read the launch's tag (workgroup 0 moves the epoch on only
+    // after seeing every mark, so no workgroup dispatched late can read the next launch's tag)
+    if (tid == 0) gput(marks + wg, tag, 0.f);
     lds_barrier();
     Ctx c{p, tag, pos, &bad_s, red_s};
     auto stamp = [&](int k) {  // diagnostic timeline (DecodePersistArgs::stamps)
         if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 128 + k] = __builtin_amdgcn_s_memrealtime();  // 100 MHz
     };
     stamp(0);
-    const int64_t slab = decode_persist_slab(H, KVH, HD, D, FD);
+    // test knob (L3_DECODE_PERSIST_FAULT): workgroup fault_wg gives up at once in the step at
+    // fault_pos (a layer workgroup after reducing the previous step's partials, as every layer
+    // workgroup does before its first wait: the previous step's id always reaches the history)
+    const bool fault = pos == p.fault_pos && wg == p.fault_wg;
     const int64_t h2_off = (int64_t)qkvn + qdim + D + FD;  // h2 within a slab
-    u64* lm_g = p.gran + slab * p.n_layers;
     const int K4d = D / 4, K4f = FD / 4, K4q = qdim / 4;
-    // roles: layer workgroup lw (the layer stages; the attention of head lw < H) or lm workgroup lwg
-    const bool layer_wg = XL ? wg % 8 == 0 : wg < p.GL;
-    const int lw = XL ? wg / 8 : wg;
+    // roles: layer workgroup (the layer stages; the attention of head wg < H) or lm workgroup lwg
+    const bool layer_wg = wg < p.GL;
 
     // lm_head rows of this workgroup: [r0, r1); unit = one row, LPR lanes.  Only the workgroups
     // past GL take rows: they load them at launch, while the layers run (rows on the layer
     // workgroups were loaded after their last stage and made the final argmax wait ~1 us)
-    const int nlm = G - p.GL, lwg = XL ? wg - wg / 8 - 1 : wg - p.GL;
+    const int nlm = G - p.GL, lwg = wg - p.GL;
     const int lm_per = (p.VS + nlm - 1) / nlm;
     const int lm_r0 = layer_wg ? p.VS : lwg * lm_per, lm_r1 = min(p.VS, lm_r0 + lm_per);
     const int lm_passes = lm_r1 > lm_r0 ? (lm_r1 - lm_r0 + UPP - 1) / UPP : 0;
     // the generate-history fields workgroup 0 writes at the end, fetched now (off the final path)
     const int hist_base = p.st->hist_base, hist_cap = p.st->hist_cap;
     int32_t* const hist = p.st->hist;
+    float* const hist_val = p.st->hist_val;
     // from_parts: the previous step (the launch before this one in the same graph) left its
     // lm_head partials and no id; every layer workgroup reduces them itself (plain loads: written
     // by the previous launch) — its final argmax hand-off and reduction come off that step's tail.
@@ -334,18 +345,18 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             bi = take ? pi[w2] : bi;
         }
         id = bi;
-        if (lw == 0 && tid == 0) {  // the previous step's id: its generate history entry
+        if (wg == 0 && tid == 0) {  // the previous step's id (and its logit): its generate history entry
             const int q = pos - 1 - hist_base;
             if (hist && q >= 0 && q < hist_cap) hist[q] = id;
+            if (hist_val && q >= 0 && q < hist_cap) hist_val[q] = best;
         }
     };
-    // XL relies on wg % 8 == 0 sharing one XCD (round-robin dealing; which XCD varies from launch
-    // to launch; the host checked the dealing once, l3::decode_persist_xcd_probe): were a layer
-    // workgroup elsewhere, its peers' XCD-local stores would not reach it and the bounded waits
-    // would end the launch with the error word set
-    if (p.stamps && tid == 0) p.stamps[(int64_t)wg * 128 + 127] = xcc_id();
     if (!layer_wg) {
         // ---- final RMSNorm + lm_head (llama3.py:304-307) + this workgroup's argmax (:320) ---------
+        if (fault) {
+            if (tid == 0) give_up(c);
+            return;
+        }
         f32x4 lw[LMPF][1][NCD];  // live on this path only (not across the layer loop)
 #pragma unroll
         for (int ps = 0; ps < LMPF; ++ps) {  // nothing else to do: the rows land while the layers run
@@ -356,11 +367,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         u64* g_last = p.gran + slab * (p.n_layers - 1) + h2_off;
         if (tid == 0) {  // a long wait: one lane polls the last granule, sleeping
             for (unsigned spin = 0; (unsigned)(gget(g_last + D - 1) >> 32) != tag; ++spin) {
-                if (spin > (1u << 20)) break;
+                if (spin > (1u << 20) || ((spin & 255) == 255 && sticky(c))) break;
                 __builtin_amdgcn_s_sleep(16);
             }
         }
-        if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, 8)) goto done;
+        if (!sweep_n(c, g_last, D, xs, [](int i) { return i; }, 8, true)) return;
         stamp(100);
         f32x4 xv[NCD];
         read_x<NCD>(xs, K4d, xv);
@@ -416,11 +427,14 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             gput(lm_g + 2 * lwg + 1, tag, __int_as_float(bi));
         }
         stamp(101);
-        goto done;
+        return;
     }
 
-
     if (p.from_parts) reduce_parts();
+    if (fault) {
+        if (tid == 0) give_up(c);
+        return;
+    }
     for (int li = 0; li < p.n_layers; ++li) {
         u64* g_qkv = p.gran + slab * li;
         u64* g_o = g_qkv + qkvn;
@@ -428,12 +442,12 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         u64* g_hid = g_h1 + D;
         u64* g_h2 = g_hid + FD;
         const float* wqkv = p.wqkv[li];
-        float* ck = p.cache_k[li];
-        float* cv = p.cache_v[li];
+        const float* ck = p.cache_k[li];
+        const float* cv = p.cache_v[li];
         // the attention workgroup's K / V rows of this layer (keys before pos: written by earlier
         // launches), fetched in stage B before its hand-off wait (fetched at the layer's start
         // instead, ahead of the QKV rows, the step measured 0.091 against 0.087 ms)
-        const int kvh = lw / (H / KVH);
+        const int kvh = wg / (H / KVH);
         // P.V layout: 16 key groups (rg, one 16-lane row each) x 16 float4 columns (d4; the ones
         // past HD / 4 idle), so a wave's four key groups reduce across its rows on the VALU
         const int D4 = HD / 4;
@@ -447,10 +461,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         const int kmax = pos > 0 ? pos - 1 : 0;
         const gf4p Kg = gf4(K4p), Vg = gf4(V4p);
         f32x4 kr[KPF], vr[VPF];
-        // ---- stage A: RMSNorm + QKV + RoPE + KV append (llama3.py:248, 166-185) -------------
+        // ---- stage A: RMSNorm + QKV + RoPE (llama3.py:248, 166-181); the K / V append
+        // (:184-185) waits for the end of the step (see the header) ----------------------------
         {
             bool valid;
-            const int u = stage_unit(p, qkvn / 2, lw, valid);  // RoPE pair (rows 2u, 2u + 1)
+            const int u = stage_unit(p, qkvn / 2, wg, valid);  // RoPE pair (rows 2u, 2u + 1)
             const int row[2] = {2 * u, 2 * u + 1};
             f32x4 w[2][NCD];
             load_rows<2, NCD>(wqkv, row, K4d, w);
@@ -463,10 +478,10 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 const int t = pos * (HD >> 1) + (d >> 1);
                 cs = float2{p.rope_cos[t], p.rope_sin[t]};
             }
-            float* cache = sec == 1 ? ck : cv;
-            const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
+            // the slot's previous contents, for the run-ahead undo (kv_bak, written at the end)
             float2 old = {0.f, 0.f};
-            if (p.kv_bak && sec > 0 && valid) old = *reinterpret_cast<const float2*>(cache + coff);
+            if (p.kv_bak && sec > 0 && valid)
+                old = *reinterpret_cast<const float2*>((sec == 1 ? ck : cv) + ((int64_t)head * p.Smax + pos) * HD + d);
             // the layer input: the token's embedding row (llama3.py:287), else the previous
             // layer's output granules
             if (li == 0) {
@@ -477,7 +492,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 if (tid < K4d) reinterpret_cast<f32x4*>(hin)[tid] = e;
                 lds_barrier();
             } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
-                goto done;
+                return;
             }
             stamp(1 + 10 * li);
             float acc[2];
@@ -486,20 +501,15 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 const float v0 = acc[0] * rs, v1 = acc[1] * rs;
                 const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
                 const float s = sec == 0 ? p.q_scale : 1.0f;
-                gput_s<XL>(g_qkv + col, tag, r0 * s);
-                gput_s<XL>(g_qkv + col + 1, tag, r1 * s);
-                if (sec > 0) {
-                    if (p.kv_bak)  // [pos % KV_BAK_SLOTS][k, v][1][KVH][HD]: the slot it overwrites
-                        *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer +
-                                                   (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d) = old;
-                    *reinterpret_cast<float2*>(cache + coff) = float2{r0, r1};
-                }
+                gput(g_qkv + col, tag, r0 * s);
+                gput(g_qkv + col + 1, tag, r1 * s);
+                if (sec > 0) kvs[li * UPP + tid / LPR] = f32x4{r0, r1, old.x, old.y};
             }
             stamp(2 + 10 * li);
         }
         // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
-        if (lw < H) {
-            const int h = lw;
+        if (wg < H) {
+            const int h = wg;
             float* qs = xs;                              // q | k_new | v_new of this head
             const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
 #pragma unroll
@@ -507,7 +517,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
 #pragma unroll
             for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + d4];
             if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
-                goto done;
+                return;
             stamp(3 + 10 * li);
             // only the K chunks past HD need zeroing (the q4 reads there land in k_new); a lane's
             // score past pos is never kept and a V row past pos never used (P.V checks k < pos),
@@ -600,184 +610,225 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             if (tid < D4) {
                 f32x4 o = (part[tid] + part[16 + tid]) + (part[32 + tid] + part[48 + tid]);
                 o *= 1.0f / l;
-                gput_s<XL>(g_o + qo + 4 * tid + 0, tag, o.x);
-                gput_s<XL>(g_o + qo + 4 * tid + 1, tag, o.y);
-                gput_s<XL>(g_o + qo + 4 * tid + 2, tag, o.z);
-                gput_s<XL>(g_o + qo + 4 * tid + 3, tag, o.w);
+                gput(g_o + qo + 4 * tid + 0, tag, o.x);
+                gput(g_o + qo + 4 * tid + 1, tag, o.y);
+                gput(g_o + qo + 4 * tid + 2, tag, o.z);
+                gput(g_o + qo + 4 * tid + 3, tag, o.w);
             }
             stamp(4 + 10 * li);
         }
         // ---- stage C: O-proj + residual (llama3.py:211, 253) --------------------------------
         {
             bool valid;
-            const int u = stage_unit(p, D, lw, valid);
+            const int u = stage_unit(p, D, wg, valid);
             const int row[1] = {u};
             f32x4 w[1][NCD];
             load_rows<1, NCD>(p.wo[li], row, K4q, w);
-            if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) goto done;
+            if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) return;
             stamp(5 + 10 * li);
             float acc[1];
             dot_rows<1, NCD>(w, xs, K4q, acc);
-            if (valid && tid % LPR == 0) gput_s<XL>(g_h1 + u, tag, hin[u] + acc[0]);
+            if (valid && tid % LPR == 0) gput(g_h1 + u, tag, hin[u] + acc[0]);
             stamp(6 + 10 * li);
         }
         // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) -----------------------
         {
             bool valid;
-            // unit u: hidden units GU u .. GU u + GU - 1; hidden unit v: fused rows 32(v/16) + v%16, +16
-            constexpr int GU = XL ? 2 : 1;
-            const int u = stage_unit(p, FD / GU, lw, valid);
-            int row[2 * GU];
-#pragma unroll
-            for (int g = 0; g < GU; ++g) {
-                const int v = GU * u + g;
-                row[2 * g] = 32 * (v / 16) + v % 16;
-                row[2 * g + 1] = row[2 * g] + 16;
-            }
-            f32x4 w[2 * GU][NCD];
-            load_rows<2 * GU, NCD>(p.wgu[li], row, K4d, w);
-            if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) goto done;
+            // unit u: hidden unit u, fused rows 32(u/16) + u%16 (gate) and +16 (up)
+            const int u = stage_unit(p, FD, wg, valid);
+            int row[2];
+            row[0] = 32 * (u / 16) + u % 16;
+            row[1] = row[0] + 16;
+            f32x4 w[2][NCD];
+            load_rows<2, NCD>(p.wgu[li], row, K4d, w);
+            if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) return;
             stamp(7 + 10 * li);
-            float acc[2 * GU];
-            const float rs = dot_rows_rms<2 * GU, NCD>(w, h1s, K4d, p.eps, acc);
+            float acc[2];
+            const float rs = dot_rows_rms<2, NCD>(w, h1s, K4d, p.eps, acc);
             if (valid && tid % LPR == 0) {
-#pragma unroll
-                for (int g = 0; g < GU; ++g) {
-                    const float gt = acc[2 * g] * rs, up = acc[2 * g + 1] * rs;
-                    gput_s<XL>(g_hid + GU * u + g, tag, gt * __builtin_amdgcn_rcpf(1.0f + __expf(-gt)) * up);
-                }
+                const float gt = acc[0] * rs, up = acc[1] * rs;
+                gput(g_hid + u, tag, gt * __builtin_amdgcn_rcpf(1.0f + __expf(-gt)) * up);
             }
             stamp(8 + 10 * li);
         }
         // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
         {
             bool valid;
-            const int u = stage_unit(p, D, lw, valid);
+            const int u = stage_unit(p, D, wg, valid);
             const int row[1] = {u};
             f32x4 w[1][NCF];
             load_rows<1, NCF>(p.wd[li], row, K4f, w);
-            if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) goto done;
+            // workgroup 0's last wait also covers every workgroup's start mark (they were written
+            // at launch: no extra round trip for the check the epoch bump needs)
+            const bool last0 = wg == 0 && li + 1 == p.n_layers;
+            const int64_t mk = marks - g_hid;
+            if (!sweep_n(c, g_hid, last0 ? FD + G : FD, xs, [=](int i) { return i < FD ? (int64_t)i : mk + (i - FD); }, 1,
+                         false, FD))
+                return;
             stamp(9 + 10 * li);
             float acc[1];
             dot_rows<1, NCF>(w, xs, K4f, acc);
-            if (valid && tid % LPR == 0) {  // the last layer's output goes to the lm workgroups
-                if (XL && li + 1 < p.n_layers) gput_xcd(g_h2 + u, tag, h1s[u] + acc[0]);
-                else gput(g_h2 + u, tag, h1s[u] + acc[0]);
-            }
+            if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);  // the last layer's: to the lm workgroups
             stamp(10 + 10 * li);
         }
     }
-    if (lw != 0) goto done;  // (wg 0 in both layouts)
+    // ---- every layer workgroup past its last wait: every stage of every layer has published ----
+    // the step's K / V rows into the caches (llama3.py:184-185), each slot's previous contents into
+    // kv_bak [pos % KV_BAK_SLOTS][k, v][1][KVH][HD] (the run-ahead undo, GemmArgs::kv_bak): stores
+    // only, from LDS (the next launch reads the rows with plain loads after the kernel boundary)
+    {
+        bool valid;
+        const int u = stage_unit(p, qkvn / 2, wg, valid);
+        const int col = 2 * u;
+        const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
+        if (valid && sec > 0 && tid % LPR == 0) {
+            const int cc = col - (sec == 1 ? qdim : qdim + kvdim);
+            const int head = cc / HD, d = cc - head * HD;
+            const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
+            const int64_t boff = (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d;
+            float* const* cache = sec == 1 ? p.cache_k : p.cache_v;
+            for (int li = 0; li < p.n_layers; ++li) {
+                const f32x4 e = kvs[li * UPP + tid / LPR];
+                if (p.kv_bak) *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer + boff) = float2{e.z, e.w};
+                *reinterpret_cast<float2*>(cache[li] + coff) = float2{e.x, e.y};
+            }
+        }
+    }
+    if (wg != 0) return;
+    // ---- workgroup 0: its last wait saw the whole chain (so every layer workgroup writes its
+    // slots) and every workgroup's start mark (every one has read this launch's tag: an lm
+    // workgroup dispatched late — another kernel holding its CU — would otherwise read the moved
+    // epoch and wait for granules no launch writes) ---------------------------------------------
+    if (tid == 0) __hip_atomic_store(p.epoch + 2, (unsigned)pos + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (!p.write_id) {
         // the next launch reduces this step's partials itself; only the position moves on here
         // (every layer workgroup read it at its start: none could have finished layer 0 else)
-        if (tid == 0) p.st->pos = pos + 1;
-        goto done;
+        if (tid == 0) {
+            p.st->pos = pos + 1;
+            *p.epoch = tag + 1;
+        }
+        return;
     }
 
-    // ---- workgroup 0, last step of a graph: the step's greedy id from the lm partials; generate history, position ----
+    // ---- (3) last step of a graph: the step's greedy id from the lm partials; generate history, position ----
     {
         float* pv = xs;  // [2 nlm]
-        if (sweep_n(c, lm_g, 2 * nlm, pv, [](int i) { return i; })) {
-            stamp(105);
-            float best = -INFINITY;
-            int bi = 0x7fffffff;
-            for (int i = tid; i < nlm; i += NT) {
-                const float v = pv[2 * i];
-                const int ix = __float_as_int(pv[2 * i + 1]);
-                const bool take = argmax_better(v, ix, best, bi);
-                best = take ? v : best;
-                bi = take ? ix : bi;
-            }
-            group_argmax<64>(best, bi, tid & 63);
-            __shared__ float fb[4];
-            __shared__ int fi[4];
-            if ((tid & 63) == 0) { fb[tid >> 6] = best; fi[tid >> 6] = bi; }
-            lds_barrier();
-            if (tid == 0) {
-                for (int w2 = 1; w2 < 4; ++w2)
-                    if (argmax_better(fb[w2], fi[w2], best, bi)) { best = fb[w2]; bi = fi[w2]; }
-                p.ids[0] = bi;
-                const int q = pos - hist_base;
-                if (hist && q >= 0 && q < hist_cap) hist[q] = bi;
-                p.st->pos = pos + 1;
-            }
-            stamp(102);
+        if (!sweep_n(c, lm_g, 2 * nlm, pv, [](int i) { return i; }, 1, true)) return;
+        stamp(105);
+        float best = -INFINITY;
+        int bi = 0x7fffffff;
+        for (int i = tid; i < nlm; i += NT) {
+            const float v = pv[2 * i];
+            const int ix = __float_as_int(pv[2 * i + 1]);
+            const bool take = argmax_better(v, ix, best, bi);
+            best = take ? v : best;
+            bi = take ? ix : bi;
         }
+        group_argmax<64>(best, bi, tid & 63);
+        __shared__ float fb[4];
+        __shared__ int fi[4];
+        if ((tid & 63) == 0) { fb[tid >> 6] = best; fi[tid >> 6] = bi; }
+        lds_barrier();
+        if (tid == 0) {
+            for (int w2 = 1; w2 < 4; ++w2)
+                if (argmax_better(fb[w2], fi[w2], best, bi)) { best = fb[w2]; bi = fi[w2]; }
+            p.ids[0] = bi;
+            const int q = pos - hist_base;
+            if (hist && q >= 0 && q < hist_cap) hist[q] = bi;
+            if (hist_val && q >= 0 && q < hist_cap) hist_val[q] = best;
+            p.st->pos = pos + 1;
+            *p.epoch = tag + 1;
+        }
+        stamp(102);
     }
-done:
-    if (wg == 0 && tid == 0) *p.epoch = tag + 1;  // every workgroup has read its last granule
 }
 
-// instantiated shapes: chunk counts rounded up (the loads past K are predicated off)
+// Instances (chunk counts rounded up; the loads past K are clamped): X(NCD, NCF, KPF, LMPF)
+#define L3_PERSIST_INSTANCES(X)                                                                   \
+    X(1, 3, 16, 8)    /* tiny models (tests) */                                                   \
+    X(5, 12, 12, 11)  /* stories15M: D 288, FD 768, HD 48 (167 lm rows per lm workgroup) */       \
+    X(5, 12, 16, 8)   /* the same D / FD with HD 52..64 (D 256: 4 heads of 64) */                 \
+    X(5, 16, 16, 4)                                                                               \
+    X(8, 16, 16, 2)                                                                               \
+    X(1, 12, 16, 8)                                                                               \
+    X(5, 3, 16, 8)                                                                                \
+    X(8, 12, 16, 2)
+
 static int ncd_of(int D) { const int n = (D + 63) / 64; return n <= 1 ? 1 : n <= 5 ? 5 : n <= 8 ? 8 : 0; }
 static int ncf_of(int FD) { const int n = (FD + 63) / 64; return n <= 3 ? 3 : n <= 12 ? 12 : n <= 16 ? 16 : 0; }
 
+// the first instance that takes the shape: its (D, FD) chunking and KPF >= HD / 4 (a KPF short of
+// HD / 4 would drop the old keys' last dims from their scores)
+struct PersistInstance { int ncd, ncf, kpf, lmpf; };
+static const PersistInstance kPersistInstances[] = {
+#define L3_ROW(A, B, C, E) {A, B, C, E},
+    L3_PERSIST_INSTANCES(L3_ROW)
+#undef L3_ROW
+};
+static const PersistInstance* persist_instance(const DecodePersistArgs& a) {
+    const int ncd = ncd_of(a.D), ncf = ncf_of(a.FD);
+    for (const PersistInstance& x : kPersistInstances)
+        if (x.ncd == ncd && x.ncf == ncf && a.HD / 4 <= x.kpf) return &x;
+    return nullptr;
+}
+
+static const void* persist_kernel(const PersistInstance* x) {
+#define L3_FN(A, B, C, E) \
+    if (x->ncd == A && x->ncf == B && x->kpf == C && x->lmpf == E) return reinterpret_cast<const void*>(&decode_persist_kernel<A, B, C, E>);
+    L3_PERSIST_INSTANCES(L3_FN)
+#undef L3_FN
+    return nullptr;
+}
+
 bool decode_persist_ok(const DecodePersistArgs& a) {
     const int qkvn = (a.H + 2 * a.KVH) * a.HD;
-    const int gu = a.xcd ? 2 : 1;  // hidden units per gate|up unit
     return a.D % 4 == 0 && a.FD % 4 == 0 && a.HD % 4 == 0 && a.HD >= 4 && a.HD <= 64 && a.H <= a.GL &&
-           a.H % a.KVH == 0 && a.H * a.HD == a.D && ncd_of(a.D) && ncf_of(a.FD) && qkvn % 2 == 0 &&
-           (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD / gu + a.GL - 1) / a.GL <= persist::UPP &&
+           a.H % a.KVH == 0 && a.H * a.HD == a.D && persist_instance(a) && qkvn % 2 == 0 &&
+           (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD + a.GL - 1) / a.GL <= persist::UPP &&
            (a.D + a.GL - 1) / a.GL <= persist::UPP && a.D / 4 <= persist::NT && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
-           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256 && (!a.xcd || a.GL == 32);
+           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256;
 }
 
-// Which XCD the workgroups of a 256-workgroup grid run on: the hardware deals workgroups to the
-// 8 XCDs round-robin (SPX mode), so wg % 8 == 0 share one — checked here once, before the
-// one-XCD layout (DecodePersistArgs::xcd) is used.
-__global__ void xcc_probe_kernel(unsigned* out) {
-    if (threadIdx.x == 0) out[blockIdx.x] = persist::xcc_id();
+static size_t persist_lds(const DecodePersistArgs& a) {  // K / V pairs, hin, h1s, xs, scores, P.V partials
+    return ((size_t)4 * persist::UPP * a.n_layers + 2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
 }
 
-int decode_persist_xcd_probe() {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 256)
-        return 0;
-    unsigned* d = nullptr;
-    unsigned h[256];
-    if (hipMalloc(&d, sizeof h) != hipSuccess) return 0;
-    bool ok = true;
-    for (int rep = 0; rep < 3 && ok; ++rep) {
-        hipLaunchKernelGGL(xcc_probe_kernel, dim3(256), dim3(256), 0, 0, d);
-        ok = hipDeviceSynchronize() == hipSuccess && hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) == hipSuccess;
-        for (int i = 0; i < 256 && ok; ++i) ok = (i % 8 == 0) == (h[i] == h[0]);
-    }
-    (void)hipFree(d);
-    return ok ? 1 : 0;
-}
-
-// Grid of one decode step: one workgroup per CU (256 on MI355X; every one resident: 1 per CU by
-// its registers), dynamic LDS sized by the shape
-hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s) {
-    if (!decode_persist_ok(a)) return hipErrorNotSupported;
+// Grid of one decode step, 0 when the step cannot run on this device: one workgroup per CU (256
+// on MI355X), every one of them resident at once — the workgroups wait on each other, so the
+// grid must not exceed the CUs times the blocks per CU the kernel's resources admit (its
+// registers hold it to 1; checked with the occupancy query at the dynamic LDS).  Fewer CUs than
+// the layer workgroups + the lm workgroups need (a CPX partition's 32) means no persistent step.
+// L3_DECODE_PERSIST_MAX_CUS caps the CU count seen (test knob).
+int decode_persist_grid(const DecodePersistArgs& a) {
+    if (!decode_persist_ok(a)) return 0;
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return hipErrorNotSupported;
+        return 0;
+    const int cap = env_knob("L3_DECODE_PERSIST_MAX_CUS", 0);
+    if (cap > 0 && cap < cus) cus = cap;
     const int grid = cus < 256 ? cus : 256;
-    if (grid <= a.GL || 2 * (grid - a.GL) > a.Xp || (a.xcd && grid != 256)) return hipErrorNotSupported;
-    // hin, h1s, xs, scores, P.V partials
-    const size_t lds = ((size_t)2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
-    if (lds > 64 * 1024) return hipErrorNotSupported;  // (the default dynamic LDS cap)
-    const int ncd = ncd_of(a.D), ncf = ncf_of(a.FD);
-#define L3_PERSIST(NCD, NCF, KPF, LMPF)                                                            \
-    if (ncd == NCD && ncf == NCF) {                                                                \
-        if (a.xcd)                                                                                 \
-            hipLaunchKernelGGL((decode_persist_kernel<NCD, NCF, KPF, LMPF, true>), dim3(grid), dim3(256), lds, s, a); \
-        else                                                                                       \
-            hipLaunchKernelGGL((decode_persist_kernel<NCD, NCF, KPF, LMPF, false>), dim3(grid), dim3(256), lds, s, a); \
-        return hipGetLastError();                                                                  \
+    if (grid <= a.GL || 2 * (grid - a.GL) > a.Xp) return 0;
+    const size_t lds = persist_lds(a);
+    if (lds > 64 * 1024) return 0;  // (the default dynamic LDS cap)
+    int per_cu = 0;
+    const void* fn = persist_kernel(persist_instance(a));
+    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu < 1)
+        return 0;
+    return grid;
+}
+
+hipError_t launch_decode_persist(const DecodePersistArgs& a, int grid, hipStream_t s) {
+    if (grid < 1 || grid > 256 || grid <= a.GL || !decode_persist_ok(a)) return hipErrorNotSupported;
+    const size_t lds = persist_lds(a);
+    const PersistInstance* x = persist_instance(a);
+#define L3_LAUNCH(A, B, C, E)                                                                            \
+    if (x->ncd == A && x->ncf == B && x->kpf == C && x->lmpf == E) {                                     \
+        hipLaunchKernelGGL((decode_persist_kernel<A, B, C, E>), dim3(grid), dim3(256), lds, s, a);      \
+        return hipGetLastError();                                                                        \
     }
-    L3_PERSIST(1, 3, 16, 8)   // tiny models (tests)
-    L3_PERSIST(5, 12, 12, 11)  // stories15M: D 288, FD 768, HD 48 (167 lm rows per lm workgroup)
-    L3_PERSIST(5, 16, 16, 4)
-    L3_PERSIST(8, 16, 16, 2)
-    L3_PERSIST(1, 12, 16, 8)
-    L3_PERSIST(5, 3, 16, 8)
-    L3_PERSIST(8, 12, 16, 2)
-#undef L3_PERSIST
+    L3_PERSIST_INSTANCES(L3_LAUNCH)
+#undef L3_LAUNCH
     return hipErrorNotSupported;
 }
 

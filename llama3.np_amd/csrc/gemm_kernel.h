@@ -800,6 +800,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
     ArgmaxPart fq[FOLD ? FU : 1];
     int f_pos = 0, f_base = 0, f_cap = 0;  // block 0: the history fields, fetched up front
     int32_t* f_hist = nullptr;
+    float* f_hist_val = nullptr;
     if constexpr (FOLD) {
 #pragma unroll
         for (int u = 0; u < FU; ++u) fq[u] = p.amax_in[min(u * 256 + tid, p.amax_in_n - 1)];
@@ -809,6 +810,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             f_base = st->hist_base;
             f_cap = st->hist_cap;
             f_hist = st->hist;
+            f_hist_val = st->hist_val;
         }
     }
     load_chunk(0);  // in flight while the input rows are staged
@@ -894,6 +896,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             // the previous step's position: its lm_head already moved pos on (pos_adv)
             const int q = f_pos - 1 - f_base;
             if (f_hist && q >= 0 && q < f_cap) f_hist[q] = bi;
+            if (f_hist_val && q >= 0 && q < f_cap) f_hist_val[q] = bv;
         }
     }
     // stage the row block (rows past Mb zero: branch-free FMA loop), SU loads in flight per

@@ -11,7 +11,10 @@ namespace l3 {
 //   runtime.hip  L3_BATCH_SPLIT (2), L3_LAST_LAYER_ALL_ROWS (0), L3_DECODE_FUSE_O (1),
 //                L3_LM_AMAX (1), L3_DECODE_FOLD_ARGMAX (1), L3_DECODE_SPECULATE (1), L3_DECODE_GRAPH_STEPS (8),
 //                L3_DECODE_GRAPH (1), L3_COMM_MODE (1), L3_COMM_PRIORITY (1), L3_GROUP_MULTI_PATH (0),
-//                L3_DECODE_PERSIST (1 all-XCD layout; 2 one-XCD layout, 0 graph)
+//                L3_DECODE_PERSIST (1 persistent step; 0 graph)
+//   test knobs   L3_DECODE_PERSIST_MAX_CUS (cap the CUs the persistent step sees), L3_DECODE_PERSIST_FAULT
+//                (a workgroup gives up in the step at that position; L3_DECODE_PERSIST_FAULT_WG which),
+//                L3_GROUP_VIRTUAL (a group's members may share one device; D2D copies for the gather)
 //   gemm.hip     L3_SPLITK (1), L3_SPLITK_CFG (0), L3_SPLITK_BLOCKS (1024), L3_SPLITK_MINKT (8),
 //                L3_GEMV_NT (1), L3_GEMV_LPU (0 = by shape), L3_GEMV_MR (by shape), L3_SKINNY (1),
 //                L3_SKINNY_MIN (9)
@@ -41,6 +44,7 @@ struct DecState {
     int hist_cap;      //   hist[(q - hist_base) * B + b] while 0 <= q - hist_base < hist_cap
     unsigned arrive;   // argmax_kernel's block arrival count (0 between launches)
     int32_t* hist;     // null: no history
+    float* hist_val;   // null, or beside hist: each step's winning logit (the value argmax picked)
 };
 
 struct GemmArgs {
@@ -245,8 +249,6 @@ __device__ __forceinline__ int start_of(const Args& p) {
 struct DecodePersistArgs {
     int D, H, KVH, HD, FD, VS, n_layers, Smax;
     int GL;                        // workgroups that run the layer stages (the others: the lm_head)
-    int xcd;                       // 1: the layer stages on one XCD (GL = 32, wg % 8 == 0), XCD-local
-                                   //    hand-offs; 0: GL = 64 workgroups over all XCDs
     int Dp, Xp;                    // LDS floats: per D-vector, per stage-input vector (multiples of 4)
     float eps, q_scale;
     const float* emb;              // [VS, D]
@@ -266,17 +268,22 @@ struct DecodePersistArgs {
                                    //    of a graph); 0: leave them for the next launch
     DecState* st;                  // pos (read; +1), generate history
     unsigned long long* gran;      // granule slabs (decode_persist.hip), zeroed at allocation
-    unsigned* epoch;               // [0] granule tag of the next launch (starts at 1); [1] sticky failure
-    unsigned* err;                 // host-mapped: set to 1 when a workgroup gave up on a hand-off
+    unsigned* epoch;               // [0] granule tag of the next launch (starts at 1); [1] sticky failure;
+                                   // [2] pos + 1 of the last step that wrote its K / V rows to the caches
+    unsigned* err;                 // host-mapped: pos + 1 of the step in which a workgroup gave up
     unsigned long long* stamps;    // diagnostic (null): [workgroup][128] s_memrealtime at stage points
+    int fault_pos, fault_wg;       // test knob: workgroup fault_wg gives up in the step at fault_pos (-1: none)
 };
 // granules per layer of the persistent step: [qkv | o | h1 | hid | h2]
 __host__ __device__ inline int64_t decode_persist_slab(int H, int KVH, int HD, int D, int FD) {
     return (int64_t)(H + 2 * KVH) * HD + (int64_t)H * HD + D + FD + D;
 }
 bool decode_persist_ok(const DecodePersistArgs& a);
-hipError_t launch_decode_persist(const DecodePersistArgs& a, hipStream_t s);
-int decode_persist_xcd_probe();  // 1: the workgroups wg % 8 == 0 of a grid share one XCD
+// the launch's grid on the current device, 0 when the step cannot run there (shape, CU count,
+// co-residency by the occupancy query at its LDS)
+int decode_persist_grid(const DecodePersistArgs& a);
+// grid: decode_persist_grid's, taken before a stream capture (no device queries inside one)
+hipError_t launch_decode_persist(const DecodePersistArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);

@@ -50,6 +50,7 @@ __device__ __forceinline__ void argmax_finish(float best, int bi, int32_t* __res
                 // before the atomic), so none sees the advanced value.
                 const int pos = st->pos - hist_off, q = pos - st->hist_base;
                 if (st->hist && q >= 0 && q < st->hist_cap) st->hist[(int64_t)q * gridDim.x + blockIdx.x] = bi;
+                if (st->hist_val && q >= 0 && q < st->hist_cap) st->hist_val[(int64_t)q * gridDim.x + blockIdx.x] = best;
                 if (hist_off) {
                     // the lm_head of this step already moved the position on
                 } else if (gridDim.x == 1) {

@@ -199,7 +199,8 @@ struct l3_ctx {
     int spec_B = 0;
     int spec_limit = 0x7fffffff;     // l3_set_decode_horizon: no step at or past this position
     // ev0 / ev1 bracket the chunk's graph launch (its device time keeps step_us current while
-    // steps are served from the queue), ev follows the ids copy (the chunk is ready)
+    // steps are served from the queue; ev0 after any wait for another context's decode graphs),
+    // ev follows the ids copy (the chunk is ready)
     struct SpecChunk { int pos0, n; hipEvent_t ev0, ev1, ev; bool done; };
     std::deque<SpecChunk> spec_q;
     std::vector<hipEvent_t> spec_free;  // event pool (timing events)
@@ -212,9 +213,11 @@ struct l3_ctx {
     DecodePersistArgs persist{};
     bool persist_ready = false;
     bool persist_graph = false;      // the captured single-step graph runs the persistent step
+    // graph-only for the rest of the context's life: a persistent step gave up on a hand-off
+    // (persist_recover) or its launch was refused inside a capture (capture_steps)
+    bool persist_off = false;
+    int64_t persist_recoveries = 0;  // steps recovered on the graph path (stats)
     hipEvent_t order_ev = nullptr;   // after this context's last decode graph (launch_decode_graph)
-    int persist_xcd_ok = -1;         // wg % 8 == 0 on one XCD (decode_persist_xcd_probe); -1: not probed
-    bool persist_xcd = false;        // this capture: the one-XCD layout (L3_DECODE_PERSIST=2)
 };
 
 // ---------------------------------------------------------------------------------------
@@ -328,7 +331,7 @@ extern "C" const char* l3_last_error(void) { return g_err.c_str(); }
 
 extern "C" int l3_version(int32_t* major, int32_t* minor) {
     if (major) *major = 0;
-    if (minor) *minor = 14;
+    if (minor) *minor = 15;
     return 0;
 }
 
@@ -359,10 +362,13 @@ struct DevOrder {
 DevOrder g_order[64];
 }  // namespace
 
-static int launch_decode_graph(l3_ctx* c, hipGraphExec_t g) {
+// before (optional): recorded between that wait and the graph, so a timing pair around the graph
+// does not count another context's queued decode work
+static int launch_decode_graph(l3_ctx* c, hipGraphExec_t g, hipEvent_t before = nullptr) {
     DevOrder& d = g_order[c->device & 63];
     std::lock_guard<std::mutex> lk(d.m);
     if (d.ev && d.owner != c) HIP_TRY(hipStreamWaitEvent(c->stream, d.ev, 0));
+    if (before) HIP_TRY(hipEventRecord(before, c->stream));
     HIP_TRY(hipGraphLaunch(g, c->stream));
     // recorded even while this is the device's only context: one created later must still wait
     // for the graphs this one has already queued (run-ahead)
@@ -990,37 +996,37 @@ extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, in
     return 0;
 }
 
-// Persistent batch-1 decode step (decode_persist.hip; the default): L3_DECODE_PERSIST=1 (layer
-// stages on 64 workgroups over all XCDs), 2 (on the 32 workgroups of one XCD, if the placement
-// probe agrees; else 1) or 0 (the 25-kernel graph), and a shape the kernel takes (decode_persist_ok).  Its buffers are made once, with the
-// stream idle.
-static bool persist_wanted(l3_ctx* c, int B) {
-    // read at every capture (captures are rare), so a process can A/B the paths
-    const int mode = env_knob("L3_DECODE_PERSIST", 1);
-    if (!mode || B != 1 || c->layers.empty() || !c->dec_state) return false;
-    if (mode == 2 && c->persist_xcd_ok < 0) c->persist_xcd_ok = decode_persist_xcd_probe();
+// Persistent batch-1 decode step (decode_persist.hip; the default, L3_DECODE_PERSIST=0: the
+// 25-kernel graph): the step's shape as the kernel sees it
+static DecodePersistArgs persist_shape(const l3_ctx* c) {
     DecodePersistArgs a{};
     a.D = c->d.dim; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads; a.HD = c->HD; a.FD = c->d.hidden_dim;
-    a.VS = c->d.vocab_size; a.n_layers = (int)c->layers.size(); a.Smax = c->d.max_seq_len;
-    a.xcd = mode == 2 && c->persist_xcd_ok == 1;
-    a.GL = a.xcd ? 32 : 64;
-    if (a.xcd && !decode_persist_ok(a)) { a.xcd = 0; a.GL = 64; }
-    c->persist_xcd = a.xcd != 0;
-    return decode_persist_ok(a);
-}
-
-static int persist_setup(l3_ctx* c) {
-    if (c->persist_ready) return 0;
-    DecodePersistArgs& a = c->persist;
-    a = DecodePersistArgs{};
-    const int nl = (int)c->layers.size();
-    a.D = c->d.dim; a.H = c->d.n_heads; a.KVH = c->d.n_kv_heads; a.HD = c->HD; a.FD = c->d.hidden_dim;
-    a.VS = c->d.vocab_size; a.n_layers = nl; a.Smax = c->d.max_seq_len; a.GL = 64;
+    a.VS = c->d.vocab_size; a.n_layers = (int)c->layers.size(); a.Smax = c->d.max_seq_len; a.GL = 64;
     a.Dp = (a.D + 3) & ~3;
     int xp = c->qkvn > a.FD ? c->qkvn : a.FD;
     if (xp < 3 * a.HD) xp = 3 * a.HD;
     if (xp < 512) xp = 512;  // the final argmax's 2 x 256 partials
     a.Xp = (xp + 3) & ~3;
+    a.fault_pos = -1;
+    return a;
+}
+
+// Chosen at every capture (captures are rare, so a process can A/B the paths): the shape, and
+// the launch conditions on THIS device — enough CUs for the layer and lm workgroups, every
+// workgroup co-resident at the step's LDS (decode_persist_grid) — so a device the step cannot
+// run on (e.g. a CPX partition's 32 CUs) captures the 25-kernel graph instead of failing
+static bool persist_wanted(l3_ctx* c, int B) {
+    const int mode = env_knob("L3_DECODE_PERSIST", 1);
+    if (!mode || c->persist_off || B != 1 || c->layers.empty() || !c->dec_state) return false;
+    return decode_persist_grid(persist_shape(c)) > 0;
+}
+
+// Its buffers, made once with the stream idle
+static int persist_setup(l3_ctx* c) {
+    if (c->persist_ready) return 0;
+    DecodePersistArgs& a = c->persist;
+    a = persist_shape(c);
+    const int nl = (int)c->layers.size();
     a.eps = c->d.norm_eps;
     a.q_scale = (float)(1.4426950408889634 / std::sqrt((double)c->HD));
     a.emb = c->emb; a.lm_head = c->lm_head; a.rope_cos = c->rope_cos; a.rope_sin = c->rope_sin;
@@ -1028,7 +1034,8 @@ static int persist_setup(l3_ctx* c) {
     const int64_t slab = decode_persist_slab(a.H, a.KVH, a.HD, a.D, a.FD);
     const size_t ptr_bytes = (size_t)6 * nl * sizeof(void*);
     const size_t gran_off = (ptr_bytes + 16 + 255) & ~(size_t)255;
-    const size_t gran_bytes = (size_t)(slab * nl + 2 * 256) * 8;
+    // per-layer slabs, the lm_head partials [2 x 256], the start marks [256]
+    const size_t gran_bytes = (size_t)(slab * nl + 3 * 256) * 8;
     HIP_TRY(hipMalloc(&c->persist_mem, gran_off + gran_bytes));
     HIP_TRY(hipMemset(c->persist_mem, 0, gran_off + gran_bytes));
     std::vector<const void*> ptrs((size_t)6 * nl);
@@ -1046,7 +1053,7 @@ static int persist_setup(l3_ctx* c) {
     a.wd = reinterpret_cast<const float* const*>(arr(3));
     a.cache_k = reinterpret_cast<float* const*>(arr(4));
     a.cache_v = reinterpret_cast<float* const*>(arr(5));
-    a.epoch = reinterpret_cast<unsigned*>(base + ptr_bytes);
+    a.epoch = reinterpret_cast<unsigned*>(base + ptr_bytes);  // [3] words (16 bytes reserved)
     const unsigned one = 1;  // tag 0 is what the zeroed slabs hold
     HIP_TRY(hipMemcpy(a.epoch, &one, sizeof one, hipMemcpyHostToDevice));
     a.gran = reinterpret_cast<unsigned long long*>(base + gran_off);
@@ -1075,10 +1082,51 @@ static void persist_dump_stamps(l3_ctx* c) {
     }
 }
 
-// after a synchronised replay: a persistent step that gave up on a hand-off left wrong ids
-static int persist_check(l3_ctx* c) {
-    if (c->persist_err && *reinterpret_cast<volatile unsigned*>(c->persist_err))
-        return fail("persistent decode step: a workgroup timed out on an in-launch hand-off");
+// after a synchronised replay / chunk: a persistent step gave up on a hand-off
+static bool persist_failed(const l3_ctx* c) {
+    return c->persist_err && *reinterpret_cast<volatile unsigned*>(c->persist_err) != 0u;
+}
+
+static void spec_drop_queue(l3_ctx* c) {
+    for (auto& q : c->spec_q) c->spec_free.insert(c->spec_free.end(), {q.ev0, q.ev1, q.ev});
+    c->spec_q.clear();
+    c->spec_base = c->spec_end = 0;
+}
+
+// Recovery from a persistent step that gave up (decode_persist.hip: its position + 1 in the error
+// word; every launch queued after it returned at once, the sticky word set).  With the stream
+// drained: the run-ahead steps nobody has taken are undone — those before the failed one in full
+// from kv_bak, the failed one only if it reached its cache write (epoch[2]; else it wrote no cache
+// slot), none after it (they never ran) — the failure words are cleared, and the context turns
+// graph-only: its decode graphs are dropped, so the caller's step runs eagerly and the next
+// capture is the 25-kernel graph.  *failed_pos: the step to run again.
+static int persist_recover(l3_ctx* c, int* failed_pos) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int fp = (int)*c->persist_err - 1;
+    unsigned w[3] = {0, 0, 0};
+    HIP_TRY(hipMemcpy(w, c->persist.epoch, sizeof w, hipMemcpyDeviceToHost));
+    const bool wrote = w[2] == (unsigned)fp + 1u;
+    const int KVH = c->d.n_kv_heads, HD = c->HD;
+    for (int pos = c->spec_base; pos < c->spec_end; ++pos) {
+        if (pos > fp || (pos == fp && !wrote)) continue;
+        const int n = c->spec_B * KVH * HD;
+        for (size_t li = 0; li < c->layers.size(); ++li) {
+            const float* bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * KVH * HD + (int64_t)(pos % KV_BAK_SLOTS) * 2 * n;
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_k, bak, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
+        }
+    }
+    spec_drop_queue(c);
+    const unsigned fresh[3] = {w[0] + 1u, 0u, 0u};  // a tag no granule carries; sticky and cache words cleared
+    HIP_TRY(hipMemcpyAsync(c->persist.epoch, fresh, sizeof fresh, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    *c->persist_err = 0;
+    c->persist_off = true;
+    drop_decode_graph(c);
+    c->persist_graph = false;
+    c->dec_pos_mirror = -1;
+    c->persist_recoveries++;
+    if (failed_pos) *failed_pos = fp;
     return 0;
 }
 
@@ -1088,44 +1136,59 @@ static int persist_check(l3_ctx* c) {
 static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGraphExec_t* exec) {
     const bool timing = c->timing;
     c->timing = false;  // no event records inside the graph
-    const bool persist = persist_wanted(c, B);
+    bool persist = persist_wanted(c, B);
     if (persist && persist_setup(c)) { c->timing = timing; return 1; }
-    HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    const int pgrid = persist ? decode_persist_grid(c->persist) : 0;
+    persist = pgrid > 0;
     int rc = 0;
-    // batch 1: each step's argmax folded into the next step's layer-0 QKV, one argmax launch per
-    // graph (its last step); the lm_heads move the position on
-    const int fold = persist ? 0 : fold_parts(c, B);
-    for (int i = 0; i < steps && persist && !rc; ++i) {  // one launch per step
-        DecodePersistArgs a = c->persist;
-        a.ids = c->dec_ids;
-        a.st = c->dec_state;
-        a.kv_bak = c->bak_capture ? c->kv_bak : nullptr;
-        a.xcd = c->persist_xcd ? 1 : 0;
-        a.GL = a.xcd ? 32 : 64;
-        a.from_parts = i > 0;            // the previous step in this graph left partials only
-        a.write_id = i == steps - 1;     // the last one publishes the id for the host / next graph
-        const hipError_t e = launch_decode_persist(a, c->stream);
-        if (e != hipSuccess) rc = fail("persistent decode step launch in capture failed: %s", hipGetErrorString(e));
-    }
-    for (int i = 0; i < steps && !persist && !rc; ++i) {
-        c->fold_in = fold && i > 0;
-        c->fold_adv = fold > 0;
-        c->fold_n = fold;
-        rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
-        c->fold_in = c->fold_adv = false;
-        if (!rc && fold && c->amax_n != fold) rc = fail("decode capture: lm_head partials %d, expected %d", c->amax_n, fold);
-        if (!rc && (!fold || i == steps - 1)) {
-            hipError_t e = launch_greedy_argmax(c, B, c->dec_state, fold ? 1 : 0);
-            if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
-        }
-    }
-    c->fold_in = c->fold_adv = false;
     hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    for (;;) {
+        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        bool refused = false;
+        for (int i = 0; i < steps && persist && !rc && !refused; ++i) {  // one launch per step
+            DecodePersistArgs a = c->persist;
+            a.ids = c->dec_ids;
+            a.st = c->dec_state;
+            a.kv_bak = c->bak_capture ? c->kv_bak : nullptr;
+            a.from_parts = i > 0;            // the previous step in this graph left partials only
+            a.write_id = i == steps - 1;     // the last one publishes the id for the host / next graph
+            a.fault_pos = env_knob("L3_DECODE_PERSIST_FAULT", -1);  // test knobs (kernels.h)
+            a.fault_wg = env_knob("L3_DECODE_PERSIST_FAULT_WG", 1);
+            refused = launch_decode_persist(a, pgrid, c->stream) != hipSuccess;
+        }
+        // batch 1 (graph path): each step's argmax folded into the next step's layer-0 QKV, one
+        // argmax launch per graph (its last step); the lm_heads move the position on
+        const int fold = persist ? 0 : fold_parts(c, B);
+        for (int i = 0; i < steps && !persist && !rc; ++i) {
+            c->fold_in = fold && i > 0;
+            c->fold_adv = fold > 0;
+            c->fold_n = fold;
+            rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
+            c->fold_in = c->fold_adv = false;
+            if (!rc && fold && c->amax_n != fold) rc = fail("decode capture: lm_head partials %d, expected %d", c->amax_n, fold);
+            if (!rc && (!fold || i == steps - 1)) {
+                hipError_t e = launch_greedy_argmax(c, B, c->dec_state, fold ? 1 : 0);
+                if (e != hipSuccess) rc = fail("argmax launch in capture failed: %s", hipGetErrorString(e));
+            }
+        }
+        c->fold_in = c->fold_adv = false;
+        g = nullptr;
+        const hipError_t e = hipStreamEndCapture(c->stream, &g);
+        if (refused) {
+            // the persistent launch was refused inside the capture: this context captures the
+            // 25-kernel graph from now on (the refusal left no work on the stream)
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            c->persist_off = true;
+            persist = false;
+            continue;
+        }
+        if (rc) { if (g) (void)hipGraphDestroy(g); c->timing = timing; return rc; }
+        if (e != hipSuccess) { c->timing = timing; return fail("hipStreamEndCapture failed: %s", hipGetErrorString(e)); }
+        break;
+    }
     c->timing = timing;
-    if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
-    if (e != hipSuccess) return fail("hipStreamEndCapture failed: %s", hipGetErrorString(e));
-    e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    hipError_t e = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
     if (e != hipSuccess) { (void)hipGraphDestroy(g); return fail("hipGraphInstantiate failed: %s", hipGetErrorString(e)); }
     *graph = g;
     return 0;
@@ -1268,8 +1331,7 @@ static int speculate(l3_ctx* c, int B) {
                 c->spec_free.pop_back();
             }
         }
-        HIP_TRY(hipEventRecord(ev[0], c->stream));
-        if (launch_decode_graph(c, k > 1 ? c->dec_exec_n : c->dec_exec)) return 1;
+        if (launch_decode_graph(c, k > 1 ? c->dec_exec_n : c->dec_exec, ev[0])) return 1;
         HIP_TRY(hipEventRecord(ev[1], c->stream));
         HIP_TRY(hipMemcpyAsync(c->spec_ids + (size_t)c->spec_end * B, c->spec_hist + (size_t)c->spec_end * B,
                                (size_t)k * B * 4, hipMemcpyDeviceToHost, c->stream));
@@ -1288,6 +1350,12 @@ static int spec_resolve(l3_ctx* c) {
     if (c->spec_q.empty()) return 0;
     HIP_TRY(hipSetDevice(c->device));
     c->gather_tail = false;  // the restores below are queued after the gather
+    // persistent steps queued: one that gave up leaves its own slot and every later one unwritten,
+    // so the undo waits for them and takes the failure into account (persist_recover)
+    if (c->persist_ready && !c->persist_off) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (persist_failed(c)) return persist_recover(c, nullptr);
+    }
     const int KVH = c->d.n_kv_heads, HD = c->HD, n = c->spec_B * KVH * HD;
     for (int pos = c->spec_base; pos < c->spec_end; ++pos) {
         for (size_t li = 0; li < c->layers.size(); ++li) {
@@ -1296,9 +1364,7 @@ static int spec_resolve(l3_ctx* c) {
             HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
         }
     }
-    for (auto& q : c->spec_q) c->spec_free.insert(c->spec_free.end(), {q.ev0, q.ev1, q.ev});
-    c->spec_q.clear();
-    c->spec_base = c->spec_end = 0;
+    spec_drop_queue(c);
     c->dec_pos_mirror = -1;
     return 0;
 }
@@ -1320,16 +1386,22 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
         bool hit = L == 1 && !logits_host && c->spec_B == B && c->spec_base == start_pos && !c->timing &&
                    (int)c->dec_last.size() == B;
         for (int i = 0; hit && i < B; ++i) hit = c->dec_last[(size_t)i] == ids_host[i];
-        if (hit) {
+        if (hit && !c->spec_q.front().done) {
             auto& q = c->spec_q.front();  // holds position spec_base
-            if (!q.done) {
-                HIP_TRY(hipEventSynchronize(q.ev));
-                q.done = true;
-                if (persist_check(c)) return 1;
+            HIP_TRY(hipEventSynchronize(q.ev));
+            q.done = true;
+            if (persist_failed(c)) {
+                // a persistent step gave up: everything queued is undone, this step runs eagerly
+                if (persist_recover(c, nullptr)) return 1;
+                hit = false;
+            } else {
                 float ms = 0.f;  // the chunk's graph time on the device, per step
                 if (hipEventElapsedTime(&ms, q.ev0, q.ev1) == hipSuccess && ms > 0.f)
                     note_step_time(c, 1e3 * (double)ms / q.n);
             }
+        }
+        if (hit) {
+            auto& q = c->spec_q.front();
             for (int i = 0; i < B; ++i) next_ids_host[i] = c->spec_ids[(size_t)start_pos * B + i];
             if (++c->spec_base == q.pos0 + q.n) {
                 c->spec_free.insert(c->spec_free.end(), {q.ev0, q.ev1, q.ev});
@@ -1348,13 +1420,18 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
     bool replay = L == 1 && !logits_host && c->dec_exec && c->dec_B == B &&
                   c->dec_pos_mirror == start_pos && (int)c->dec_last.size() == B && !c->timing;
     for (int i = 0; replay && i < B; ++i) replay = c->dec_last[(size_t)i] == ids_host[i];
+    double t0_replay = 0.0;
     if (replay) {
-        const double t0 = now_us();
+        t0_replay = now_us();
         if (launch_decode_graph(c, c->dec_exec)) return 1;
         HIP_TRY(hipMemcpyAsync(c->dec_host, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if (persist_check(c)) return 1;
-        note_step_time(c, now_us() - t0);
+        // a persistent step that gave up: recovered, then this step runs eagerly below
+        if (persist_failed(c) && persist_recover(c, nullptr)) return 1;
+        replay = c->dec_exec != nullptr;
+    }
+    if (replay) {
+        note_step_time(c, now_us() - t0_replay);
         for (int i = 0; i < B; ++i) next_ids_host[i] = c->dec_host[i];
         c->dec_last.assign(next_ids_host, next_ids_host + B);
         c->dec_pos_mirror = start_pos + 1;
@@ -1395,9 +1472,10 @@ extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B
 // then decode step i >= 1 at pos = L + i, each step one replay of the captured decode graph;
 // ids accumulate on the device and come back with one copy at the end.  Not lazy: all
 // max_new_tokens - L steps run (Llama.generate keeps the reference's one-step-per-yield).
-extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
-                                       int32_t max_new_tokens, int64_t* out_ids_host) {
-    CHECK_CTX(c);
+// out_vals (optional, [B, steps]): each step's winning logit, the value its argmax picked (the
+// graph steps record it beside the id; the two eager steps read it from their logits rows).
+static int greedy_generate(l3_ctx* c, const int64_t* ids_host, int B, int L, int max_new_tokens,
+                           int64_t* out_ids_host, float* out_vals) {
     const int steps = max_new_tokens - L;
     if (steps <= 0) return 0;
     // the last decode step runs at position max_new_tokens - 1, which must be a cache slot
@@ -1413,24 +1491,39 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
         explicit InLoop(l3_ctx* x) : c(x) { c->in_loop = true; }
         ~InLoop() { c->in_loop = false; }
     } in_loop(c);
+    const int64_t VS = c->d.vocab_size;
+    std::vector<float> lg(out_vals ? (size_t)B * VS : 0);
+    // an eager step's values: its logits row at the id it returned
+    auto eager_vals = [&](const int64_t* ids, int row) {
+        if (!out_vals) return;
+        for (int b = 0; b < B; ++b) out_vals[(size_t)b * steps + row] = lg[(size_t)b * VS + ids[b]];
+    };
     std::vector<int64_t> first((size_t)B);
-    if (l3_greedy_step_host(c, ids_host, B, L, 0, first.data(), nullptr)) return 1;  // prefill
+    if (l3_greedy_step_host(c, ids_host, B, L, 0, first.data(), out_vals ? lg.data() : nullptr)) return 1;  // prefill
+    eager_vals(first.data(), 0);
     if (steps == 1) {
         for (int b = 0; b < B; ++b) out_ids_host[(size_t)b * steps] = first[(size_t)b];
         return 0;
     }
     // decode step 1 at pos L + 1 runs eagerly and arms the graph (device ids, pos = L + 2)
     std::vector<int64_t> nxt((size_t)B);
-    if (l3_greedy_step_host(c, first.data(), B, 1, L + 1, nxt.data(), nullptr)) return 1;
+    if (l3_greedy_step_host(c, first.data(), B, 1, L + 1, nxt.data(), out_vals ? lg.data() : nullptr)) return 1;
+    eager_vals(nxt.data(), 1);
     int32_t* hist = nullptr;
+    float* hval = nullptr;
     HIP_TRY(hipMalloc(&hist, (size_t)steps * B * 4));
+    if (out_vals && hipMalloc(&hval, (size_t)steps * B * 4) != hipSuccess) {
+        (void)hipFree(hist);
+        return fail("generate: value history allocation failed");
+    }
     // the captured argmax writes each replayed step's ids straight into hist (DecState: the
     // step at position L + i is row i), so the loop is graph launches only
-    auto set_hist = [&](int32_t* ptr, int base, int cap) {
+    auto set_hist = [&](int32_t* ptr, float* vptr, int base, int cap) {
         DecState h{};
         h.hist_base = base;
         h.hist_cap = cap;
         h.hist = ptr;
+        h.hist_val = vptr;
         const size_t off = offsetof(DecState, hist_base);
         if (hipMemcpyAsync(reinterpret_cast<char*>(c->dec_state) + off, reinterpret_cast<char*>(&h) + off,
                            sizeof(DecState) - off, hipMemcpyHostToDevice, c->stream) != hipSuccess)
@@ -1438,9 +1531,10 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
         return hipStreamSynchronize(c->stream) == hipSuccess;  // h is on this stack frame
     };
     auto done = [&](int rc) {
-        (void)set_hist(nullptr, 0, 0);
+        (void)set_hist(nullptr, nullptr, 0, 0);
         (void)hipStreamSynchronize(c->stream);
         (void)hipFree(hist);
+        if (hval) (void)hipFree(hval);
         return rc;
     };
     std::vector<int32_t> h32((size_t)B);
@@ -1448,7 +1542,7 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
     if (hipMemcpy(hist, h32.data(), (size_t)B * 4, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpyAsync(hist + B, c->dec_ids, (size_t)B * 4, hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
         return done(fail("generate: history copy failed"));
-    if (steps > 2 && !set_hist(hist, L, steps)) return done(fail("generate: decode state update failed"));
+    if (steps > 2 && !set_hist(hist, hval, L, steps)) return done(fail("generate: decode state update failed"));
     // the graph replays only from the state the eager step above armed (position L + 2)
     if (steps > 2 && (!c->dec_exec || c->dec_B != B || c->dec_pos_mirror != L + 2))
         return done(fail("generate: decode graph not armed"));
@@ -1462,17 +1556,59 @@ extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32
         c->graph_steps += multi ? n : 1;
     }
     std::vector<int32_t> all((size_t)steps * B);
+    std::vector<float> vals(out_vals ? (size_t)steps * B : 0);
     if (hipMemcpyAsync(all.data(), hist, all.size() * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        (out_vals && hipMemcpyAsync(vals.data(), hval, vals.size() * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess) ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return done(fail("generate: copy-back failed"));
-    if (persist_check(c)) return done(1);
+    int from = steps;  // rows [2, from) are the device loop's
+    if (persist_failed(c)) {
+        // a persistent step gave up at position fp = L + k: rows before k stand; the rest run on
+        // the graph path, one call per step (the first eager at the failed position, then replays)
+        int fp = 0;
+        if (persist_recover(c, &fp)) return done(1);
+        const int k = fp - L;
+        if (k < 2 || k >= steps) return done(fail("generate: persistent step failed at position %d, outside [%d, %d)", fp, L + 2, L + steps));
+        from = k;
+        std::vector<int64_t> in((size_t)B), nx((size_t)B);
+        for (int i = k; i < steps; ++i) {
+            for (int b = 0; b < B; ++b) in[(size_t)b] = all[(size_t)(i - 1) * B + b];
+            const bool eager = i == k;  // the replays record their values in hval, like the loop's
+            if (l3_greedy_step_host(c, in.data(), B, 1, L + i, nx.data(), eager && out_vals ? lg.data() : nullptr))
+                return done(1);
+            if (eager) eager_vals(nx.data(), i);
+            for (int b = 0; b < B; ++b) all[(size_t)i * B + b] = (int32_t)nx[(size_t)b];
+        }
+        if (out_vals && k + 1 < steps &&
+            (hipMemcpyAsync(vals.data() + (size_t)(k + 1) * B, hval + (size_t)(k + 1) * B, (size_t)(steps - k - 1) * B * 4,
+                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             hipStreamSynchronize(c->stream) != hipSuccess))
+            return done(fail("generate: copy-back failed"));
+    }
     persist_dump_stamps(c);
     for (int i = 0; i < steps; ++i)
         for (int b = 0; b < B; ++b) out_ids_host[(size_t)b * steps + i] = all[(size_t)i * B + b];
+    for (int i = 2; out_vals && i < steps; ++i) {
+        if (i == from) continue;  // the eager step's own
+        for (int b = 0; b < B; ++b) out_vals[(size_t)b * steps + i] = vals[(size_t)i * B + b];
+    }
     c->dec_last.assign(B, 0);
     for (int b = 0; b < B; ++b) c->dec_last[(size_t)b] = all[(size_t)(steps - 1) * B + b];
     c->dec_pos_mirror = L + steps;  // the device state now expects position L + steps
     return done(0);
+}
+
+extern "C" int l3_greedy_generate_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
+                                       int32_t max_new_tokens, int64_t* out_ids_host) {
+    CHECK_CTX(c);
+    return greedy_generate(c, ids_host, B, L, max_new_tokens, out_ids_host, nullptr);
+}
+
+extern "C" int l3_greedy_generate_values_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
+                                              int32_t max_new_tokens, int64_t* out_ids_host, float* out_vals) {
+    CHECK_CTX(c);
+    if (!out_vals) return fail("l3_greedy_generate_values_host: null out_vals");
+    return greedy_generate(c, ids_host, B, L, max_new_tokens, out_ids_host, out_vals);
 }
 
 extern "C" int l3_layer_forward_host(l3_ctx* c, int32_t layer, const float* x_host, int32_t B,
@@ -1745,6 +1881,12 @@ extern "C" int l3_set_decode_horizon(l3_ctx* c, int32_t end_pos) {
 extern "C" int l3_decode_persistent(l3_ctx* c, int32_t* active) {
     CHECK_CTX(c);
     if (active) *active = c->dec_exec && c->persist_graph ? 1 : 0;
+    return 0;
+}
+
+extern "C" int l3_decode_recoveries(l3_ctx* c, int64_t* count) {
+    CHECK_CTX(c);
+    if (count) *count = c->persist_recoveries;
     return 0;
 }
 
@@ -2022,6 +2164,12 @@ struct l3_group {
     // n > 1, or n = 1 with L3_GROUP_MULTI_PATH=1 (tests: the 1-GPU box runs it against the
     // single-device path); otherwise every call is member 0's own
     bool multi = false;
+    // L3_GROUP_VIRTUAL=1 (test knob): members may share a device, no communicators; the gather's
+    // point-to-point transfers become device copies into the same member-0 buffers, ordered by
+    // events, so the row split, the offsets and the interleave run for real on one GPU
+    bool virt = false;
+    std::vector<hipEvent_t> rows_ev; // virt: member i's rows written (recorded on its stream)
+    hipEvent_t copied_ev = nullptr;  // virt: member 0 has copied every member's rows
     std::vector<l3_ctx*> m;
     std::vector<ncclComm_t> comms;
     std::vector<int> devs;
@@ -2054,6 +2202,8 @@ extern "C" int l3_group_destroy(l3_group* g) {
     if (!g->m.empty() && g->m[0]) {
         (void)hipSetDevice(g->m[0]->device);
         dfree(g->gbuf); dfree(g->gout); dfree(g->gids);
+        for (hipEvent_t e : g->rows_ev) if (e) (void)hipEventDestroy(e);
+        if (g->copied_ev) (void)hipEventDestroy(g->copied_ev);
     }
     for (size_t i = 0; i < g->comms.size(); ++i)
         if (g->comms[i]) { (void)hipSetDevice(g->devs[i]); ncclCommDestroy(g->comms[i]); }
@@ -2067,10 +2217,12 @@ extern "C" int l3_group_create(int32_t ndev, const int32_t* devices, const l3_di
     if (!devices || !dims || !out) return fail("l3_group_create: null argument");
     int have = 0;
     HIP_TRY(hipGetDeviceCount(&have));
-    if (ndev < 1 || ndev > have) return fail("l3_group_create: %d devices requested, %d present", ndev, have);
+    const bool virt = env_knob("L3_GROUP_VIRTUAL", 0) != 0;
+    if (ndev < 1 || (ndev > have && !virt) || ndev > 64)
+        return fail("l3_group_create: %d devices requested, %d present", ndev, have);
     for (int i = 0; i < ndev; ++i) {
         if (devices[i] < 0 || devices[i] >= have) return fail("l3_group_create: no device %d", devices[i]);
-        for (int j = 0; j < i; ++j)
+        for (int j = 0; j < i && !virt; ++j)
             if (devices[j] == devices[i]) return fail("l3_group_create: device %d listed twice", devices[i]);
     }
     if (dims->max_batch_size < 1) return fail("l3_group_create: max_batch_size %d < 1", dims->max_batch_size);
@@ -2079,6 +2231,7 @@ extern "C" int l3_group_create(int32_t ndev, const int32_t* devices, const l3_di
     g->d = *dims;
     g->devs.assign(devices, devices + ndev);
     g->multi = ndev > 1 || env_knob("L3_GROUP_MULTI_PATH", 0) != 0;
+    g->virt = virt;
     l3_dims local = *dims;  // each member holds the KV cache of its rows only
     local.max_batch_size = (dims->max_batch_size + ndev - 1) / ndev;
     g->m.assign((size_t)ndev, nullptr);
@@ -2089,7 +2242,17 @@ extern "C" int l3_group_create(int32_t ndev, const int32_t* devices, const l3_di
             return fail("l3_group_create: member %d (device %d): %s", i, devices[i], e.c_str());
         }
     g->comms.assign((size_t)ndev, nullptr);
-    const ncclResult_t r = ncclCommInitAll(g->comms.data(), ndev, g->devs.data());
+    if (virt) {
+        HIP_TRY(hipSetDevice(devices[0]));
+        g->rows_ev.assign((size_t)ndev, nullptr);
+        for (int i = 0; i < ndev; ++i) {
+            HIP_TRY(hipSetDevice(devices[i]));
+            HIP_TRY(hipEventCreateWithFlags(&g->rows_ev[(size_t)i], hipEventDisableTiming));
+        }
+        HIP_TRY(hipSetDevice(devices[0]));
+        HIP_TRY(hipEventCreateWithFlags(&g->copied_ev, hipEventDisableTiming));
+    }
+    const ncclResult_t r = virt ? ncclSuccess : ncclCommInitAll(g->comms.data(), ndev, g->devs.data());
     if (r != ncclSuccess) {
         g->comms.assign((size_t)ndev, nullptr);
         l3_group_destroy(g);
@@ -2175,26 +2338,51 @@ static int group_launch(l3_group* g, const int64_t* ids_host, const int32_t* con
 template <typename T>
 static int group_gather(l3_group* g, int B, int64_t each, T** src, T* peer_buf, T* dst, ncclDataType_t type) {
     l3_ctx* c0 = g->m[0];
-    NCCL_TRY(ncclGroupStart());
-    int64_t off = 0;
-    for (int i = 1; i < g->n; ++i) {
-        const int64_t nb = group_rows(g, B, i);
-        if (!nb) continue;
-        ncclResult_t r = ncclRecv(peer_buf + off * each, (size_t)(nb * each), type, i, g->comms[0], c0->stream);
-        if (r == ncclSuccess)
-            r = ncclSend(src[i], (size_t)(nb * each), type, 0, g->comms[(size_t)i], g->m[(size_t)i]->stream);
-        if (r != ncclSuccess) {
-            (void)ncclGroupEnd();
-            return fail("group gather (member %d): %s", i, ncclGetErrorString(r));
+    if (g->virt) {
+        // the same transfers as device copies on member 0's stream: after each member's rows are
+        // written (its event), into the same peer_buf offsets; the members' next writes of their
+        // rows wait for the copies (RCCL's send completes on the sender's stream the same way)
+        int64_t voff = 0;
+        for (int i = 1; i < g->n; ++i) {
+            const int64_t nb = group_rows(g, B, i);
+            if (!nb) continue;
+            l3_ctx* ci = g->m[(size_t)i];
+            HIP_TRY(hipSetDevice(ci->device));
+            HIP_TRY(hipEventRecord(g->rows_ev[(size_t)i], ci->stream));
+            HIP_TRY(hipSetDevice(c0->device));
+            HIP_TRY(hipStreamWaitEvent(c0->stream, g->rows_ev[(size_t)i], 0));
+            HIP_TRY(hipMemcpyAsync(peer_buf + voff * each, src[i], (size_t)(nb * each) * sizeof(T), hipMemcpyDeviceToDevice,
+                                   c0->stream));
+            voff += nb;
         }
-        off += nb;
+        HIP_TRY(hipEventRecord(g->copied_ev, c0->stream));
+        for (int i = 1; i < g->n; ++i) {
+            if (!group_rows(g, B, i)) continue;
+            HIP_TRY(hipSetDevice(g->m[(size_t)i]->device));
+            HIP_TRY(hipStreamWaitEvent(g->m[(size_t)i]->stream, g->copied_ev, 0));
+        }
+    } else {
+        NCCL_TRY(ncclGroupStart());
+        int64_t off = 0;
+        for (int i = 1; i < g->n; ++i) {
+            const int64_t nb = group_rows(g, B, i);
+            if (!nb) continue;
+            ncclResult_t r = ncclRecv(peer_buf + off * each, (size_t)(nb * each), type, i, g->comms[0], c0->stream);
+            if (r == ncclSuccess)
+                r = ncclSend(src[i], (size_t)(nb * each), type, 0, g->comms[(size_t)i], g->m[(size_t)i]->stream);
+            if (r != ncclSuccess) {
+                (void)ncclGroupEnd();
+                return fail("group gather (member %d): %s", i, ncclGetErrorString(r));
+            }
+            off += nb;
+        }
+        NCCL_TRY(ncclGroupEnd());
     }
-    NCCL_TRY(ncclGroupEnd());
     HIP_TRY(hipSetDevice(c0->device));
     const size_t pitch = (size_t)g->n * each * sizeof(T), w = (size_t)each * sizeof(T);
     HIP_TRY(hipMemcpy2DAsync(dst, pitch, src[0], w, w, (size_t)group_rows(g, B, 0), hipMemcpyDeviceToDevice,
                              c0->stream));
-    off = 0;
+    int64_t off = 0;
     for (int i = 1; i < g->n; ++i) {
         const int64_t nb = group_rows(g, B, i);
         if (!nb) continue;

@@ -63,6 +63,7 @@ _SIGNATURES = {
     "l3_greedy_step_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "l3_layer_forward_host": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P]),
     "l3_greedy_generate_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
+    "l3_greedy_generate_values_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P, _P]),
     "l3_attention_forward_host": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _I32, _P]),
     "l3_op_softmax_host": (ctypes.c_int, [_P, _P, _I64, _I64, _P]),
     "l3_op_argmax_host": (ctypes.c_int, [_P, _P, _I64, _I64, _P]),
@@ -82,6 +83,7 @@ _SIGNATURES = {
     "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
     "l3_decode_stats": (ctypes.c_int, [_P, _P, _P]),
     "l3_decode_persistent": (ctypes.c_int, [_P, _P]),
+    "l3_decode_recoveries": (ctypes.c_int, [_P, _P]),
     "l3_set_decode_horizon": (ctypes.c_int, [_P, _I32]),
     "l3_comm_unique_id": (ctypes.c_int, [_P]),
     "l3_comm_init": (ctypes.c_int, [_P, _I32, _I32, _P]),
@@ -116,7 +118,10 @@ def lib() -> ctypes.CDLL:
                 f"libllama3hip.so not found at {LIB_PATH}: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
         so = ctypes.CDLL(LIB_PATH)
+        other = bool(os.environ.get("L3_LIB_PATH"))  # an older A/B build may lack newer entry points
         for name, (res, args) in _SIGNATURES.items():
+            if other and not hasattr(so, name):
+                continue
             fn = getattr(so, name)
             fn.restype = res
             fn.argtypes = args
@@ -299,12 +304,18 @@ class Context:
                                         ptr(logits) if logits is not None else None))
         return nxt, logits
 
-    def greedy_generate(self, ids: np.ndarray, max_new_tokens: int) -> np.ndarray:
+    def greedy_generate(self, ids: np.ndarray, max_new_tokens: int, values: bool = False):
+        """The device-side greedy loop: ids [B, max_new_tokens - L]; with ``values`` also each
+        step's winning logit (fp32, same shape) — the value the step's argmax picked."""
         ids = np.ascontiguousarray(ids, dtype=np.int64)
         B, L = ids.shape
         out = np.empty((B, max(0, max_new_tokens - L)), np.int64)
-        check(lib().l3_greedy_generate_host(self._h, ptr(ids), B, L, max_new_tokens, ptr(out)))
-        return out
+        if not values:
+            check(lib().l3_greedy_generate_host(self._h, ptr(ids), B, L, max_new_tokens, ptr(out)))
+            return out
+        vals = np.empty(out.shape, np.float32)
+        check(lib().l3_greedy_generate_values_host(self._h, ptr(ids), B, L, max_new_tokens, ptr(out), ptr(vals)))
+        return out, vals
 
     def layer_forward(self, layer: int, x: np.ndarray, start_pos: int) -> np.ndarray:
         x = np.ascontiguousarray(x, dtype=np.float32)
@@ -377,6 +388,12 @@ class Context:
         v = ctypes.c_int32(0)
         check(lib().l3_decode_persistent(self._h, ctypes.byref(v)))
         return bool(v.value)
+
+    def decode_recoveries(self) -> int:
+        """Persistent decode steps that gave up on a hand-off and were re-run on the graph path."""
+        v = ctypes.c_int64(0)
+        check(lib().l3_decode_recoveries(self._h, ctypes.byref(v)))
+        return int(v.value)
 
     def decode_stats(self) -> dict:
         """Decode steps served by graph replay, and of those by a speculative step."""

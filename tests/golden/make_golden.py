@@ -110,14 +110,16 @@ def model_fixture(tmp, name, args, hidden, seed, preset, cases, gen=None):
     if gen is not None:
         gtag, gids, max_new = gen
         gm = ref.Llama(path, ref_args(args))
-        steps, margins = [], []
-        # replicate Llama.generate but also record the top-2 margin of each step
+        steps, margins, maxes = [], [], []
+        # replicate Llama.generate but also record the top-2 margin and the winning logit of
+        # each step
         L = gids.shape[1]
         nxt = None
         for i, pos in enumerate(range(L, max_new)):
             logits = gm(gids, 0) if i == 0 else gm(nxt, pos)
             srt = np.sort(logits[:, -1, :], axis=-1)
             margins.append(srt[:, -1] - srt[:, -2])
+            maxes.append(srt[:, -1])
             nxt = logits[:, -1, :].argmax(-1, keepdims=True)
             steps.append(nxt)
         ids_ref = np.concatenate(list(ref.Llama(path, ref_args(args)).generate(gids, max_new)), axis=1)
@@ -127,6 +129,7 @@ def model_fixture(tmp, name, args, hidden, seed, preset, cases, gen=None):
         out[f"{gtag}_max_new"] = np.int64(max_new)
         out[f"{gtag}_ids"] = got
         out[f"{gtag}_margin"] = np.stack(margins, axis=1)
+        out[f"{gtag}_max"] = np.stack(maxes, axis=1)  # the logit np.argmax picked, per step
         # decode hole: layer-0 cache rows that are still exactly zero after generate
         ck = gm.layers[0].attention.cache_k
         out[f"{gtag}_zero_slots"] = np.nonzero(np.all(ck[0] == 0, axis=(1, 2)))[0][:8]

@@ -1,0 +1,192 @@
+"""The persistent batch-1 decode step (decode_persist.hip) as every batch-1 user's default path:
+values pinned against the reference, not only ids; the launch gated on the device it runs on;
+a step that gives up on an in-launch hand-off recovered on the 25-kernel graph path with the
+reference's result; the HD = 64 instance.
+
+Reference: llama3.py:304-321 (final norm, lm_head, greedy argmax, the generate schedule with
+its decode hole).  Fixtures: tests/golden/stories15m_{default,sharp}.npz, made by running the
+reference itself (tests/golden/make_golden.py): 145 greedy ids of "I have a dream", and per
+step the winning logit (dream_max) and the top-2 margin (dream_margin).
+"""
+
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+import llama3
+import llama3_oracle as orc
+import synth
+from config import ModelArgs
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+ATOL, RTOL = 1e-4, 2e-4  # north star 1e-4; the sharp preset: the reference test's own form
+
+
+@pytest.fixture(scope="module")
+def tmpdir_mod():
+    with tempfile.TemporaryDirectory() as d:
+        yield d
+
+
+def _stories(tmp, preset):
+    g = load_golden(f"stories15m_{preset}")
+    args = synth.stories15m(1)
+    path = os.path.join(tmp, f"s15_{preset}.npz")
+    if not os.path.exists(path):
+        synth.save_npz(path, synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=int(g["seed"]), preset=preset))
+    return g, args, path
+
+
+def _dream(g):
+    return (np.asarray(g["dream_prompt"]).reshape(1, -1), np.asarray(g["dream_ids"]).reshape(1, -1),
+            int(g["dream_max_new"]))
+
+
+@pytest.mark.parametrize("persist", ["1", "0"])
+@pytest.mark.parametrize("preset", ["default", "sharp"])
+def test_decode_values_match_reference(tmpdir_mod, monkeypatch, preset, persist):
+    """Each greedy step's winning logit (the value np.argmax picked, llama3.py:320) against the
+    reference's, over all 145 steps: the persistent step (one launch per step, values from its
+    lm_head partials) and the 25-kernel graph (values from its argmax kernels), in the device
+    loop.  Default preset: within 1e-4; sharp (|logits| ~ 33): 1e-4 + 2e-4 |ref|.  Reports the
+    smallest top-2 margin of the run (the reference's), i.e. how close an id came to flipping."""
+    monkeypatch.setenv("L3_DECODE_PERSIST", persist)
+    g, args, path = _stories(tmpdir_mod, preset)
+    prompt, want, n = _dream(g)
+    m = llama3.Llama(path, args)
+    ids, vals = m.context.greedy_generate(prompt, n, values=True)
+    np.testing.assert_array_equal(ids, want)
+    assert m.context.decode_persistent() == (persist == "1")
+    ref = np.asarray(g["dream_max"]).reshape(1, -1)
+    err = np.abs(vals.astype(np.float64) - ref)
+    tol = ATOL + (RTOL * np.abs(ref) if preset == "sharp" else 0.0)
+    assert (err <= tol).all(), f"worst step {int(err.argmax())}: {err.max():.3e}"
+    margin = np.asarray(g["dream_margin"])
+    print(f"{preset} persist={persist}: max-abs {err.max():.2e} over {ref.size} steps, "
+          f"|logit| <= {np.abs(ref).max():.2f}, smallest top-2 margin {margin.min():.2e} at step {int(margin.argmin())}")
+    # the ids-only entry point is the same loop
+    m2 = llama3.Llama(path, args)
+    np.testing.assert_array_equal(m2.generate_all(prompt, n), want)
+
+
+def test_persistent_decode_needs_its_cus(tmpdir_mod, monkeypatch):
+    """A device with fewer CUs than the step's layer + lm workgroups (a CPX partition has 32;
+    L3_DECODE_PERSIST_MAX_CUS=32 makes this device look like one) captures the 25-kernel graph
+    instead of failing: the device loop, the lazy generator and an abandoned generator all give
+    the reference's 145 ids."""
+    g, args, path = _stories(tmpdir_mod, "default")
+    prompt, want, n = _dream(g)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    monkeypatch.setenv("L3_DECODE_PERSIST_MAX_CUS", "32")
+    m = llama3.Llama(path, args)
+    np.testing.assert_array_equal(m.generate_all(prompt, n), want)
+    assert not m.context.decode_persistent()
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
+    assert not m.context.decode_persistent()
+    # with every CU visible again the next capture is the persistent step
+    monkeypatch.delenv("L3_DECODE_PERSIST_MAX_CUS")
+    m2 = llama3.Llama(path, args)
+    np.testing.assert_array_equal(m2.generate_all(prompt, n), want)
+    assert m2.context.decode_persistent()
+
+
+# (fault position, workgroup that gives up): a layer workgroup at the step's start — no stage
+# completes, the step writes no cache slot — or an lm workgroup — the layers complete and the
+# step writes its K / V slots before the launch fails (epoch[2]), so an undo must restore them
+FAULTS = [(30, 1), (41, 255)]
+
+
+@pytest.mark.parametrize("fault_pos,fault_wg", FAULTS)
+def test_persistent_decode_fault_recovers_device_loop(tmpdir_mod, monkeypatch, fault_pos, fault_wg):
+    """One workgroup gives up in the step at fault_pos (L3_DECODE_PERSIST_FAULT, inside an 8-step
+    graph of the device loop): every later launch of the graph returns at once; the loop
+    recovers — clears the failure words, turns the context graph-only — and runs the rest from
+    the failed position on the 25-kernel graph.  145 / 145 ids and every step's value equal the
+    reference's, no exception, and the context is graph-only afterwards."""
+    g, args, path = _stories(tmpdir_mod, "sharp")
+    prompt, want, n = _dream(g)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", str(fault_pos))
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
+    m = llama3.Llama(path, args)
+    ids, vals = m.context.greedy_generate(prompt, n, values=True)
+    np.testing.assert_array_equal(ids, want)
+    ref = np.asarray(g["dream_max"]).reshape(1, -1)
+    assert (np.abs(vals - ref) <= ATOL + RTOL * np.abs(ref)).all()
+    assert m.context.decode_recoveries() == 1
+    assert not m.context.decode_persistent()
+    # the context stays correct (graph path) for the next calls
+    np.testing.assert_array_equal(m.generate_all(prompt, n), want)
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
+
+
+@pytest.mark.parametrize("fault_pos,fault_wg", FAULTS)
+def test_persistent_decode_fault_recovers_lazy(tmpdir_mod, monkeypatch, fault_pos, fault_wg):
+    """The same fault under the lazy generator with run-ahead (llama3.py:310-321: one step per
+    yield, the device up to 16 steps ahead): the step that finds the failure undoes every
+    queued step — those before the failed one in full, the failed one if it wrote its slots,
+    none after it — and runs eagerly; the generator yields the reference's 145 ids.  Then an
+    abandoned generator (run-ahead undone on the graph path) and a full one: the KV caches the
+    recovery left behind give the reference's ids again."""
+    g, args, path = _stories(tmpdir_mod, "sharp")
+    prompt, want, n = _dream(g)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", str(fault_pos))
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
+    m = llama3.Llama(path, args)
+    got = np.concatenate(list(m.generate(prompt, n)), axis=1)
+    np.testing.assert_array_equal(got, want)
+    assert m.context.decode_recoveries() == 1
+    assert not m.context.decode_persistent()
+    gen = m.generate(prompt, n)
+    for _ in range(20):
+        next(gen)
+    del gen
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
+
+
+def test_persistent_decode_fault_in_abandoned_run_ahead(tmpdir_mod, monkeypatch):
+    """The fault lands in a step the device ran ahead: the consumer stops before it (an
+    abandoned generator).  Whichever call finds the failure — a served step's chunk sync, or the
+    next call's undo of the abandoned run-ahead (spec_resolve) — restores only the slots the
+    steps that ran wrote, and the following full generation is exact."""
+    g, args, path = _stories(tmpdir_mod, "sharp")
+    prompt, want, n = _dream(g)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", "20")
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", "255")
+    m = llama3.Llama(path, args)
+    gen = m.generate(prompt, n)
+    first = [next(gen) for _ in range(10)]  # positions 5..14 handed out; 15.. queued ahead
+    np.testing.assert_array_equal(np.concatenate(first, axis=1), want[:, :10])
+    del gen
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
+    assert m.context.decode_recoveries() == 1
+
+
+def test_persistent_decode_hd64_instance(tmpdir_mod, monkeypatch):
+    """Head dim 64 with D <= 320 and FD in (192, 768] (D 256 = 4 heads of 64, GQA n_rep 2): the
+    (D, FD) chunking of stories15M but more old-key dims than its instance holds (KPF 12 = 48
+    dims) — the instance table picks KPF 16.  Greedy ids of the persistent step (device loop and
+    lazy) equal the oracle's and the 25-kernel graph's."""
+    args = ModelArgs(dim=256, n_layers=2, n_heads=4, n_kv_heads=2, vocab_size=512, max_seq_len=96,
+                     max_batch_size=1)
+    w = synth.make_weights(args, 512, seed=7, preset="sharp")
+    path = os.path.join(tmpdir_mod, "hd64.npz")
+    synth.save_npz(path, w)
+    prompt = np.random.default_rng(3).integers(0, args.vocab_size, (1, 7))
+    n = 80
+    want = orc.greedy_ids(orc.OracleModel(w, args), prompt, n)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    m = llama3.Llama(path, args)
+    np.testing.assert_array_equal(m.generate_all(prompt, n), want)
+    assert m.context.decode_persistent()
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "0")
+    m0 = llama3.Llama(path, args)
+    np.testing.assert_array_equal(m0.generate_all(prompt, n), want)
+    assert not m0.context.decode_persistent()
