@@ -691,6 +691,17 @@ def main():
     # value: the product forward (batch split into row ranges on concurrent streams), no events
     elapsed, elapsed_min = timed_steps(a.steps)
 
+    # beside `value` (BASELINE.md's plan: the median step): the same steps one at a time, each
+    # bracketed by a device sync — the median of those, whose gaps the back-to-back mean hides
+    per_step = []
+    for _ in range(a.steps):
+        sync()
+        t0 = time.perf_counter()
+        step()
+        sync()
+        per_step.append(time.perf_counter() - t0)
+    median_ms = dist.max(float(np.median(per_step))) * 1e3
+
     # N > 1: the gathered rows against rank 0's own recomputation (untimed)
     if a.single_process:
         checked = check_gathered_group(ctx, N, bpg, VS, gathered_dev, ids_blk) if N > 1 else None
@@ -775,6 +786,10 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "timing": (f"value and ms_per_step: wall clock of {a.steps} back-to-back steps after {a.warmup} "
+                   "warm-up steps, bracketed by a barrier and a device sync, max over ranks, mean per step; "
+                   "ms_per_step_median: the median of the same steps run one at a time, each between syncs"),
+        "ms_per_step_median": round(median_ms, 4),
         "ms_per_step_serialized": round(elapsed_serial / a.steps * 1e3, 4),
         "ms_per_step_all_rows_last_layer": round(elapsed_all_rows / a.steps * 1e3, 4),
         "batch_split": a.split if a.split is not None else 2,

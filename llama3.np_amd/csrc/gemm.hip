@@ -154,15 +154,33 @@ bool gemv_direct(const GemmArgs& a) {
 
 // 9..256 rows against a small weight on the skinny MFMA kernel (gemm_kernel.h); L3_SKINNY=0
 // keeps them on the GEMV (A/B)
-// CH = 2 k-blocks per round trip, TN = 2 column tiles past 128 rows (SwiGLU: always, the gate /
-// up pair); TN and CH leave every element's K order as it is, so all of them round identically
+// CH = 2 k-blocks per round trip, TN = 2 column tiles only for SwiGLU (the gate / up pair); TN and
+// CH leave every element's K order as it is, so all of them round identically
 // (tools/gemm_tune 5 50 skinny: at M = 64 / 128 / 256 CH 2 beat the earlier CH 6 by 10-30 %)
 template <int EPI, int TN>
 static hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
     constexpr int WN = 16 * TN;
     const int64_t blocks = (int64_t)((a.M + 15) / 16) * ((a.N + WN - 1) / WN);
-    hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    // k-blocks per round trip: 2.  In the batched decode loop (weights from MALL, not the L2-hot
+    // loop of tools/gemm_tune) CH 6 / 12 measured 0.333 / 0.408 ms per B = 256 step against 0.313
+    // (profiles/r05_skinny_ab.txt); L3_SKINNY_CH re-runs that A/B
+    static const int ch = env_knob("L3_SKINNY_CH", 2);
+    if (ch >= 12)
+        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 12>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else if (ch >= 6)
+        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 6>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
     return hipGetLastError();
+}
+
+// rows past which QKV / O-proj / down take 2-tile columns: none up to 256 (one-tile columns give
+// the 256-row launches twice the blocks: B = 256 decode 0.308-0.309 against 0.313-0.315 ms per step,
+// profiles/r05_skinny_ab.txt; the column tiling leaves each element's K order, so results are
+// bit-identical); L3_SKINNY_TN2_MIN re-runs that A/B
+static int skinny_tn2() {
+    static const int m = env_knob("L3_SKINNY_TN2_MIN", 256);
+    return m;
 }
 
 static bool use_skinny(const GemmArgs& a) {
@@ -201,6 +219,9 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
         }
     }
     if (a.amax_part && (epi != EPI_STORE || !gemv_store_blocks(a))) return hipErrorInvalidValue;
+    // amax_rows: the tiled EPI_STORE kernels only (16 * TN = 64-column wave tiles, no split-K)
+    if (a.amax_rows && (epi != EPI_STORE || gemm_store_config(a) == 0 || a.ws || a.amax_nct != (a.N + 63) / 64))
+        return hipErrorInvalidValue;
     if (a.pos_adv && !a.amax_part) return hipErrorInvalidValue;
     if (a.amax_in) {  // layer-0 QKV of a captured batch-1 decode step with the previous argmax folded in
         if (epi != EPI_QKV || a.M != 1 || !gemv_direct(a) || a.col_base || a.a_rows || a.amax_in_n < 1 ||
@@ -215,8 +236,8 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     if (a.force_skinny || (gemm_is_gemv(a) && use_skinny(a))) {
         switch (epi) {
             case EPI_SWIGLU: return launch_skinny<EPI_SWIGLU, 2>(a, s);
-            case EPI_QKV: return a.M > 128 ? launch_skinny<EPI_QKV, 2>(a, s) : launch_skinny<EPI_QKV, 1>(a, s);
-            case EPI_RESID: return a.M > 128 ? launch_skinny<EPI_RESID, 2>(a, s) : launch_skinny<EPI_RESID, 1>(a, s);
+            case EPI_QKV: return a.M > skinny_tn2() ? launch_skinny<EPI_QKV, 2>(a, s) : launch_skinny<EPI_QKV, 1>(a, s);
+            case EPI_RESID: return a.M > skinny_tn2() ? launch_skinny<EPI_RESID, 2>(a, s) : launch_skinny<EPI_RESID, 1>(a, s);
             case EPI_STORE: return launch_skinny<EPI_STORE, 1>(a, s);
             default: return hipErrorInvalidValue;
         }

@@ -170,6 +170,34 @@ __device__ __forceinline__ void direct_epilogue(const GemmArgs& p, const f32x4 (
                                                 const float (&rs)[TM], const f32x4 (&res)[NR],
                                                 int mrow0, int ncol0, int lane) {
     const int frow = lane & 15, fq4 = 4 * (lane >> 4);
+    if constexpr (EPI == EPI_STORE) {
+        if (p.amax_rows) {
+            // greedy argmax partials instead of the logits (llama3.py:320 over this wave's 16 * TN
+            // columns of each row): the lane's own columns in rising order ("strictly greater, or
+            // the first NaN" keeps the first index on ties), then the four lanes of the row
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = mrow0 + i * 16 + frow;
+                float best = -INFINITY;
+                int bi = 0x7fffffff;
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int col = ncol0 + j * 16 + fq4 + r;
+                        const float v = acc[i][j][r] * rs[i];
+                        const bool vn = v != v, bn = best != best;
+                        const bool take = col < p.N && (bi == 0x7fffffff || v > best || (vn && !bn));
+                        best = take ? v : best;
+                        bi = take ? col : bi;
+                    }
+                argmax_xor16_32<true, true>(best, bi, lane);
+                if (lane < 16 && row < p.M)
+                    p.amax_rows[(int64_t)row * p.amax_nct + ncol0 / (16 * TN)] = ArgmaxPart{best, bi};
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int row = mrow0 + i * 16 + frow;

@@ -84,6 +84,10 @@ struct GemmArgs {
     // EPI_STORE on the one-row GEMV (batch-1 lm_head): also the block's (value, index) argmax
     // over its columns -> amax_part[blockIdx.x], reduced by launch_argmax_parts
     ArgmaxPart* amax_part;
+    // EPI_STORE on the tiled kernel (a captured batched decode step's lm_head): instead of the
+    // logits, each wave's (value, index) argmax over its 64 columns of every row ->
+    // amax_rows[row][column tile], amax_nct tiles per row (C is not written)
+    ArgmaxPart* amax_rows; int amax_nct;
     DecState* pos_adv;             // ... and block 0 moves the decode position on (a captured step
                                    // whose argmax the next step's layer-0 QKV folds in)
     // EPI_QKV on the one-row GEMV (a captured batch-1 decode step after the first of a graph): the
@@ -183,6 +187,28 @@ template <int CTRL>
 __device__ __forceinline__ int dpp_mov_i(int v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
 }
+// the argmax of lanes l and l ^ 16 (X16), then of l and l ^ 32 (X32): lane i of a swapped pair
+// holds {own, lane ^ 16} with the partner second in rows 0, 2
+template <bool X16, bool X32>
+__device__ __forceinline__ void argmax_xor16_32(float& best, int& bi, int lane) {
+    auto step = [&](float ov, int oi) {
+        const bool t = argmax_better(ov, oi, best, bi);
+        best = t ? ov : best;
+        bi = t ? oi : bi;
+    };
+    if constexpr (X16) {
+        const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+        const auto x = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
+        const bool hi = lane & 16;
+        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
+    }
+    if constexpr (X32) {
+        const auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
+        const auto x = __builtin_amdgcn_permlane32_swap((unsigned)bi, (unsigned)bi, false, false);
+        const bool hi = lane & 32;
+        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
+    }
+}
 template <int LANES>
 __device__ __forceinline__ void group_argmax(float& best, int& bi, int lane) {
     auto step = [&](float ov, int oi) {
@@ -194,18 +220,7 @@ __device__ __forceinline__ void group_argmax(float& best, int& bi, int lane) {
     step(__int_as_float(dpp_mov_i<0x4E>(__float_as_int(best))), dpp_mov_i<0x4E>(bi));
     step(__int_as_float(dpp_mov_i<0x141>(__float_as_int(best))), dpp_mov_i<0x141>(bi));
     step(__int_as_float(dpp_mov_i<0x140>(__float_as_int(best))), dpp_mov_i<0x140>(bi));
-    if constexpr (LANES >= 32) {  // lane i of the swapped pair: {own, lane ^ 16}, partner second in rows 0, 2
-        const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(best), __float_as_uint(best), false, false);
-        const auto x = __builtin_amdgcn_permlane16_swap((unsigned)bi, (unsigned)bi, false, false);
-        const bool hi = lane & 16;
-        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
-    }
-    if constexpr (LANES >= 64) {
-        const auto v = __builtin_amdgcn_permlane32_swap(__float_as_uint(best), __float_as_uint(best), false, false);
-        const auto x = __builtin_amdgcn_permlane32_swap((unsigned)bi, (unsigned)bi, false, false);
-        const bool hi = lane & 32;
-        step(__uint_as_float(hi ? v[0] : v[1]), (int)(hi ? x[0] : x[1]));
-    }
+    argmax_xor16_32<LANES >= 32, LANES >= 64>(best, bi, lane);
 }
 
 // row r of A (identity, or the gathered embedding row)
@@ -290,9 +305,10 @@ hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_attention_last(const AttnArgs& a, hipStream_t s);
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,
                          DecState* st = nullptr);
-// the same result from the lm_head's per-block partials (one row: GemmArgs::amax_part)
+// the same result from the lm_head's partials: rows x nparts (GemmArgs::amax_part, one row;
+// GemmArgs::amax_rows, a batch)
 hipError_t launch_argmax_parts(const ArgmaxPart* parts, int nparts, int32_t* out, hipStream_t s,
-                               DecState* st = nullptr, int hist_off = 0);
+                               DecState* st = nullptr, int hist_off = 0, int rows = 1);
 // blocks of the one-row lm_head GEMV (= its partial count when amax_part is set), 0 otherwise
 int gemv_store_blocks(const GemmArgs& a);
 // true when launch_gemm runs this shape on the row-blocked GEMV (short M)

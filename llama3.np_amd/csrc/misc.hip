@@ -110,6 +110,7 @@ __global__ void __launch_bounds__(1024) argmax_parts_kernel(const ArgmaxPart* __
                                                             DecState* __restrict__ st, int hist_off) {
     constexpr int NT = 1024, U = 4;
     const int tid = threadIdx.x;
+    parts += (int64_t)blockIdx.x * n;  // row blockIdx.x
     float best = -INFINITY;
     int bi = 0x7fffffff;
     for (int base = 0; base < n; base += NT * U) {
@@ -197,8 +198,8 @@ hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out,
     return hipGetLastError();
 }
 hipError_t launch_argmax_parts(const ArgmaxPart* parts, int nparts, int32_t* out, hipStream_t s,
-                               DecState* st, int hist_off) {
-    hipLaunchKernelGGL(argmax_parts_kernel, dim3(1), dim3(1024), 0, s, parts, nparts, out, st, hist_off);
+                               DecState* st, int hist_off, int rows) {
+    hipLaunchKernelGGL(argmax_parts_kernel, dim3(rows), dim3(1024), 0, s, parts, nparts, out, st, hist_off);
     return hipGetLastError();
 }
 hipError_t launch_softmax(const float* x, float* y, int64_t rows, int n, hipStream_t s) {

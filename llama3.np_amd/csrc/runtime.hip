@@ -117,6 +117,11 @@ struct l3_ctx {
     int64_t skws_cap = 0;            //   with D or FD >= 2048; gemm.hip launch_split), floats
     ArgmaxPart* amax_part = nullptr; // batch-1 lm_head's per-block argmax partials
     int amax_n = 0;                  // partials the last lm_head wrote (0: none, use the logits)
+    // captured batched decode steps: the tiled lm_head writes per-row argmax partials [B][ceil(VS/64)]
+    // instead of the logits (GemmArgs::amax_rows), reduced by one B-row argmax launch
+    ArgmaxPart* amax_rows = nullptr;
+    int amax_rows_n = 0;             // partials per row the last lm_head wrote (0: none)
+    bool rows_amax = false;          // capture_steps: the lm_head may leave partials only
     int32_t *ids = nullptr, *amax = nullptr;
     int32_t* ids_pin = nullptr;      // pinned host staging of the int32 ids (upload_ids)
     int64_t ids_pin_n = 0;
@@ -298,7 +303,8 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     c->gather_tail = false;
     drop_decode_graph(c);  // the captured graph holds workspace pointers
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits);
-    dfree(c->ids); dfree(c->amax); dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum);
+    dfree(c->ids); dfree(c->amax); dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum); dfree(c->amax_rows);
+    c->amax_rows = nullptr;
     c->oparts = nullptr;
     c->hsum = nullptr;
     c->amax_part = nullptr;
@@ -317,6 +323,7 @@ static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
         HIP_TRY(hipMalloc(&c->hsum, (int64_t)8 * D * 4));
     }
     HIP_TRY(hipMalloc(&c->amax_part, ((int64_t)c->d.vocab_size / 4 + 64) * sizeof(ArgmaxPart)));
+    HIP_TRY(hipMalloc(&c->amax_rows, Bn * (((int64_t)c->d.vocab_size + 63) / 64) * sizeof(ArgmaxPart)));
     if (!c->skws && (c->d.dim >= 2048 || c->d.hidden_dim >= 2048)) {
         c->skws_cap = (int64_t)16 << 20;  // 64 MB: gate|up at M = 256 in 2 slices fits
         HIP_TRY(hipMalloc(&c->skws, c->skws_cap * 4));
@@ -465,7 +472,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     }
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
-    dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum); dfree(c->skws);
+    dfree(c->oparts); dfree(c->amax_part); dfree(c->hsum); dfree(c->skws); dfree(c->amax_rows);
     dfree(c->amax); dfree(c->gather_ids);
     if (c->ids_pin) (void)hipHostFree(c->ids_pin);
     for (void* p : c->scratch) dfree(p);
@@ -811,6 +818,10 @@ static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipSt
     c->amax_n = lm_amax_on() && b0 == 0 ? gemv_store_blocks(lm) : 0;
     if (c->amax_n) lm.amax_part = c->amax_part;
     if (c->amax_n && c->fold_adv) lm.pos_adv = c->dec_state;
+    // a captured batched decode step (ids only): argmax partials per row instead of the logits
+    c->amax_rows_n = c->rows_amax && B > 1 && b0 == 0 && !c->amax_n && gemm_store_config(lm) != 0
+                         ? (int)((c->d.vocab_size + 63) / 64) : 0;
+    if (c->amax_rows_n) { lm.amax_rows = c->amax_rows; lm.amax_nct = c->amax_rows_n; }
     return timed_on(c, L3_K_LMHEAD, s, [&] { return launch_gemm(EPI_STORE, lm, s); });
 }
 
@@ -818,6 +829,7 @@ static int run_lm_head(l3_ctx* c, int B, int L, float* logits_dev, int b0, hipSt
 // lm_head's partials when it wrote them; hist_off 1 when that lm_head moved the position on
 static hipError_t launch_greedy_argmax(l3_ctx* c, int B, DecState* st, int hist_off = 0) {
     if (c->amax_n && B == 1) return launch_argmax_parts(c->amax_part, c->amax_n, c->dec_ids, c->stream, st, hist_off);
+    if (c->amax_rows_n) return launch_argmax_parts(c->amax_rows, c->amax_rows_n, c->dec_ids, c->stream, st, 0, B);
     return launch_argmax(c->logits, B, c->d.vocab_size, c->dec_ids, c->stream, st);
 }
 
@@ -1159,12 +1171,17 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
         // batch 1 (graph path): each step's argmax folded into the next step's layer-0 QKV, one
         // argmax launch per graph (its last step); the lm_heads move the position on
         const int fold = persist ? 0 : fold_parts(c, B);
+        // batched steps: the lm_head leaves per-row argmax partials, not logits (nobody reads a
+        // captured step's logits); L3_DECODE_ROWS_AMAX=0 keeps the logits + full-row argmax (A/B)
+        static const bool rows_amax = env_knob("L3_DECODE_ROWS_AMAX", 1) != 0;
         for (int i = 0; i < steps && !persist && !rc; ++i) {
             c->fold_in = fold && i > 0;
             c->fold_adv = fold > 0;
             c->fold_n = fold;
+            c->rows_amax = rows_amax && B > 1;
             rc = forward_dev(c, c->dec_ids, B, 1, 0, c->logits, c->dec_pos);
             c->fold_in = c->fold_adv = false;
+            c->rows_amax = false;
             if (!rc && fold && c->amax_n != fold) rc = fail("decode capture: lm_head partials %d, expected %d", c->amax_n, fold);
             if (!rc && (!fold || i == steps - 1)) {
                 hipError_t e = launch_greedy_argmax(c, B, c->dec_state, fold ? 1 : 0);
@@ -1172,6 +1189,7 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
             }
         }
         c->fold_in = c->fold_adv = false;
+        c->rows_amax = false;
         g = nullptr;
         const hipError_t e = hipStreamEndCapture(c->stream, &g);
         if (refused) {

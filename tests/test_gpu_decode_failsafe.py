@@ -190,3 +190,39 @@ def test_persistent_decode_hd64_instance(tmpdir_mod, monkeypatch):
     m0 = llama3.Llama(path, args)
     np.testing.assert_array_equal(m0.generate_all(prompt, n), want)
     assert not m0.context.decode_persistent()
+
+
+def _oracle_greedy_values(ref, prompt, max_new):
+    """The reference's greedy loop (llama3.py:310-321) on the oracle, with each step's winning
+    logit (the value np.argmax picked at :320)."""
+    ids, vals, nxt = [], [], None
+    L = prompt.shape[1]
+    for i, pos in enumerate(range(L, max_new)):
+        logits = ref(prompt, 0) if i == 0 else ref(nxt, pos)
+        last = logits[:, -1, :]
+        nxt = last.argmax(-1)[:, None]
+        ids.append(nxt)
+        vals.append(last.max(-1)[:, None])
+    return np.concatenate(ids, axis=1), np.concatenate(vals, axis=1)
+
+
+@pytest.mark.parametrize("B", [16, 64, 256])
+def test_batched_decode_lm_head_partials(tmpdir_mod, B):
+    """Batched device loop (B > 8: the tiled lm_head) whose captured steps leave per-row argmax
+    partials instead of the logits (GemmArgs::amax_rows) and reduce them in one B-row launch: the
+    ids and each step's winning logit of three spread rows equal the oracle's (rows never
+    interact, llama3.py:163-211), every row's ids equal a second run's."""
+    args = synth.stories15m(B)
+    path = os.path.join(tmpdir_mod, f"b{B}.npz")
+    w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=11, preset="sharp")
+    synth.save_npz(path, w)
+    prompt = np.random.default_rng(B).integers(0, args.vocab_size, (B, 5))
+    n = 30
+    m = llama3.Llama(path, args)
+    ids, vals = m.context.greedy_generate(prompt, n, values=True)
+    for r in (0, B // 2, B - 1):
+        ref = orc.OracleModel(w, synth.stories15m(1))
+        want, wv = _oracle_greedy_values(ref, prompt[r:r + 1], n)
+        np.testing.assert_array_equal(ids[r:r + 1], want, err_msg=f"row {r}")
+        assert (np.abs(vals[r:r + 1] - wv) <= ATOL + RTOL * np.abs(wv)).all(), f"row {r}"
+    np.testing.assert_array_equal(llama3.Llama(path, args).generate_all(prompt, n), ids)
