@@ -20,6 +20,35 @@ import llama3  # noqa: E402
 import synth  # noqa: E402
 
 
+PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_TBS = 8.0        # HBM3E
+
+
+def step_roofline(args, B, L, steps, step_s):
+    """Algorithmic work of one batched greedy step averaged over the run (llama3.py:163-211,
+    304-307 at L = 1): GEMM FLOPs (QKV, O-proj, gate|up, down per layer; the lm_head), and the
+    bytes a step must move at least — every weight once, each row's K / V rows 0..pos once, its
+    new K / V slot written, the embedding rows — against the fp32 MFMA peak and HBM bandwidth.
+    The step is bound by neither: it is ~31 dependent launches of a few us each."""
+    D, H, KVH, HD, VS, nl = args.dim, args.n_heads, args.kv_heads, args.dim // args.n_heads, args.vocab_size, args.n_layers
+    FD = synth.STORIES15M_HIDDEN
+    qkvn = (H + 2 * KVH) * HD
+    w_layer = D * qkvn + D * H * HD + D * 2 * FD + FD * D
+    flops = 2.0 * B * (nl * w_layer + D * VS)
+    mean_pos = L + (steps + 1) / 2.0  # decode step i at pos L + i (the reference's schedule)
+    kv = nl * B * (4.0 * 2 * KVH * HD * (mean_pos + 1) + 4.0 * 2 * KVH * HD)
+    weights = 4.0 * (nl * w_layer + VS * D)
+    bytes_ = weights + kv + 4.0 * B * D
+    tf = flops / step_s / 1e12
+    tbs = bytes_ / step_s / 1e12
+    floor_us = max(flops / (PEAK_FP32_TFLOPS * 1e12), bytes_ / (PEAK_HBM_TBS * 1e12)) * 1e6
+    return {"flops_per_step": flops, "bytes_per_step": bytes_, "kv_bytes_per_step": kv,
+            "weight_bytes_per_step": weights, "achieved_tflops": round(tf, 2),
+            "mfma_frac": round(tf / PEAK_FP32_TFLOPS, 4), "achieved_tbs": round(tbs, 3),
+            "hbm_frac": round(tbs / PEAK_HBM_TBS, 4), "floor_us": round(floor_us, 1),
+            "step_us": round(step_s * 1e6, 1), "frac_of_floor": round(floor_us / (step_s * 1e6), 4)}
+
+
 def main():
     eager = "--eager" in sys.argv  # profiling: every step eager, no device-loop leg
     if eager:
@@ -82,8 +111,10 @@ def main():
         t0 = time.perf_counter()
         out = mb.generate_all(pr, int(g["dream_max_new"]))
         tb = time.perf_counter() - t0
+        steps = out.shape[1]
         batched[str(B)] = {"generated_tokens_per_s": round(out.size / tb, 1),
-                           "ms_per_step": round(tb / out.shape[1] * 1e3, 3)}
+                           "ms_per_step": round(tb / steps * 1e3, 3),
+                           "roofline": step_roofline(argsb, B, prompt.shape[1], steps, tb / steps)}
         del mb
     print(json.dumps({"workload": "stories15M greedy decode B=1, 'I have a dream', 145 steps",
                       "tokens_per_s_reference_count": round(count / t, 1),
