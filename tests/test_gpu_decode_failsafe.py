@@ -206,12 +206,12 @@ def _oracle_greedy_values(ref, prompt, max_new):
     return np.concatenate(ids, axis=1), np.concatenate(vals, axis=1)
 
 
-@pytest.mark.parametrize("B", [16, 64, 256])
+@pytest.mark.parametrize("B", [9, 16, 64, 256])
 def test_batched_decode_lm_head_partials(tmpdir_mod, B):
-    """Batched device loop (B > 8: the tiled lm_head) whose captured steps leave per-row argmax
-    partials instead of the logits (GemmArgs::amax_rows) and reduce them in one B-row launch: the
-    ids and each step's winning logit of three spread rows equal the oracle's (rows never
-    interact, llama3.py:163-211), every row's ids equal a second run's."""
+    """Batched device loop (B > 8: the tiled lm_head, whose captured steps leave per-row argmax
+    partials instead of the logits, GemmArgs::amax_rows, reduced in one B-row launch): the ids
+    and each step's winning logit of three spread rows equal the oracle's (rows never interact,
+    llama3.py:163-211), every row's ids equal a second run's."""
     args = synth.stories15m(B)
     path = os.path.join(tmpdir_mod, f"b{B}.npz")
     w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=11, preset="sharp")
