@@ -32,7 +32,7 @@ st[:, 127] = 0
 t0 = st[:, 0][st[:, 0] > 0].min()
 us = lambda x: (x - t0) / 100.0  # noqa: E731
 names = ["qkv", "attn", "oproj", "gateup", "down"]
-lay_idx = np.nonzero(st[:, 1] > 0)[0]  # layer workgroups (0..63, or wg % 8 == 0 in the one-XCD layout)
+lay_idx = np.arange(64)  # layer workgroups (GL = 64; fold: 0..5 the heads)
 lm_idx = np.setdiff1d(np.arange(256), lay_idx)
 lay = st[lay_idx]
 
@@ -59,5 +59,9 @@ print("attention workgroups, layer 1: in / scores / max / sum / PV / part stored
 for h in range(6):
     print("  head", h, " ".join(f"{us(st[lay_idx[h], k]):7.2f}" for k in (13, 110, 111, 112, 113, 114, 14)))
 print("layer workgroups' XCDs:", sorted(set(xcc[lay_idx].tolist())), " lm workgroups' XCDs:", sorted(set(xcc[lm_idx].tolist())))
+if st[0, 120] > 0:
+    print("fold head workgroups, layer 1: h2 in / QKV dot done / K, V requested + barrier / RoPE done / attention in")
+    for h in range(6):
+        print("  head", h, " ".join(f"{us(st[h, k]):7.2f}" for k in (11, 120, 121, 122, 13)))
 for k, nm in ((105, "wg0 partials in"), (102, "greedy id")):
     print(f"  {nm}: {us(st[0, k]):.2f}")
