@@ -209,8 +209,7 @@ int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits
  * than the 25-kernel graph.  The persistent step is the default for shapes it takes (HD <= 64,
  * decode_persist_ok) on devices it can run on (every one of its workgroups resident: enough CUs,
  * checked at capture; otherwise the graph is captured); env L3_DECODE_PERSIST (read at capture):
- * 1 default, 0 the graph; L3_DECODE_PERSIST_FOLD=1 the fold layout where the shape has one
- * (*active = 2 then: the head workgroups compute their own q / k / v rows).  A persistent step that gives up on an in-launch hand-off is recovered,
+ * 1 default, 0 the graph.  A persistent step that gives up on an in-launch hand-off is recovered,
  * not reported: the steps queued ahead are undone, the step runs again on the graph path with
  * the same result, and the context stays on the graph path (l3_decode_recoveries counts this). */
 int l3_decode_persistent(l3_ctx* ctx, int32_t* active);

@@ -246,21 +246,13 @@ __device__ __forceinline__ float dot_row_x(const f32x4 (&w)[NC], const f32x4 (&x
 
 // this workgroup's unit range of a layer stage with n units over GL workgroups (one pass: the
 // eligibility keeps ceil(n / GL) <= UPP)
-__device__ __forceinline__ int stage_unit_of(int n, int wg, int nwg, bool& valid) {
-    const int per = (n + nwg - 1) / nwg;
+__device__ __forceinline__ int stage_unit(const DecodePersistArgs& p, int n, int wg, bool& valid) {
+    const int per = (n + p.GL - 1) / p.GL;
     const int i = threadIdx.x / LPR;
     const int u = wg * per + i;
     valid = i < per && u < n;
     return valid ? u : 0;
 }
-__device__ __forceinline__ int stage_unit(const DecodePersistArgs& p, int n, int wg, bool& valid) {
-    return stage_unit_of(n, wg, p.GL, valid);
-}
-
-// fold: LDS pieces (1 KB, one global_load_lds wave-instruction each) of a head's q / k / v rows
-// held in LDS — every row but the last frp passes' (UPP rows each), which the units hold in
-// registers (3 HD = 16 FNP rows)
-__host__ __device__ inline int fold_pieces(int D, int HD, int frp) { return ((3 * HD - UPP * frp) * D * 4 + 1023) / 1024; }
 
 }  // namespace persist
 
@@ -269,7 +261,7 @@ __host__ __device__ inline int fold_pieces(int D, int HD, int frp) { return ((3 
 // NCD / NCF: float4 per lane of a W row with K = D / K = FD (>= ceil(K / 64)); KPF >= HD / 4 (the
 // old keys' chunks each attention lane holds); LMPF: lm_head passes of 16 rows each workgroup
 // holds in registers.
-template <int NCD, int NCF, int KPF, int LMPF, int FNP, int FRP, int FPW>
+template <int NCD, int NCF, int KPF, int LMPF>
 __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArgs p) {
     using namespace persist;
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -365,17 +357,9 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             if (tid == 0) give_up(c);
             return;
         }
-        // the rows are needed only at the end of the step: requested p.lm_delay ticks (100 MHz)
-        // after the launch, so the layer workgroups' first loads are not queued behind 37 MB
-        // (and pass ps p.lm_gap ticks after pass ps - 1: the 37 MB as a trickle over the layers)
-        const u64 t0 = __builtin_amdgcn_s_memrealtime();
         f32x4 lw[LMPF][1][NCD];  // live on this path only (not across the layer loop)
 #pragma unroll
         for (int ps = 0; ps < LMPF; ++ps) {  // nothing else to do: the rows land while the layers run
-            if (p.lm_delay > 0 || p.lm_gap > 0) {
-                const u64 until = (u64)p.lm_delay + (u64)ps * (u64)p.lm_gap;
-                while (__builtin_amdgcn_s_memrealtime() - t0 < until) __builtin_amdgcn_s_sleep(8);
-            }
             const int r = lm_r0 + ps * UPP + tid / LPR;
             const int row[1] = {min(r, p.VS - 1)};
             load_rows<1, NCD>(p.lm_head, row, K4d, lw[ps]);  // clamped rows
@@ -451,560 +435,262 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         if (tid == 0) give_up(c);
         return;
     }
-    const int D4 = HD / 4;
-    // P.V layout: 16 key groups (rg, one 16-lane row each) x 16 float4 columns (d4; the ones
-    // past HD / 4 idle), so a wave's four key groups reduce across its rows on the VALU
-    constexpr int R = NT / 16;
-    constexpr int VPF = NT / R;  // V rows per lane: the first NT keys
-    const int rg = tid >> 4, d4 = min(tid & 15, D4 - 1);
-    // row pos - 1 is the last one an earlier launch wrote (pos >= 1 in a decode step)
-    const int kmax = pos > 0 ? pos - 1 : 0;
-    // the old K / V rows of kv head kvh of layer li into registers (keys before pos: written by
-    // earlier launches; unpredicated loads from clamped rows, see load_rows, zeroed where used)
-    // (lane indices as arguments: the fold path passes opaque copies, see there)
-    auto load_kv = [&](const float* ck, const float* cv, int kvh, f32x4 (&kr)[KPF], f32x4 (&vr)[VPF], const int tid,
-                       const int rg, const int d4) {
-        const gf4p Kg = gf4(ck + (int64_t)kvh * p.Smax * HD), Vg = gf4(cv + (int64_t)kvh * p.Smax * HD);
-#pragma unroll
-        for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
-#pragma unroll
-        for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + d4];
-    };
-    // ---- attention of head h (llama3.py:186-210) on qs = q | k_new | v_new (LDS, RoPE'd, q
-    // scaled), the old rows in kr / vr; publishes o into g_o ---------------------------------------
-    auto attend = [&](int li, int h, const float* ck, const float* cv, const float* qs, float* sc, f32x4 (&kr)[KPF],
-                      f32x4 (&vr)[VPF], u64* g_o, const int tid, const int rg, const int d4) {
-        const int kvh = h / (H / KVH);
+    for (int li = 0; li < p.n_layers; ++li) {
+        u64* g_qkv = p.gran + slab * li;
+        u64* g_o = g_qkv + qkvn;
+        u64* g_h1 = g_o + qdim;
+        u64* g_hid = g_h1 + D;
+        u64* g_h2 = g_hid + FD;
+        const float* wqkv = p.wqkv[li];
+        const float* ck = p.cache_k[li];
+        const float* cv = p.cache_v[li];
+        // the attention workgroup's K / V rows of this layer (keys before pos: written by earlier
+        // launches), fetched in stage B before its hand-off wait (fetched at the layer's start
+        // instead, ahead of the QKV rows, the step measured 0.091 against 0.087 ms)
+        const int kvh = wg / (H / KVH);
+        // P.V layout: 16 key groups (rg, one 16-lane row each) x 16 float4 columns (d4; the ones
+        // past HD / 4 idle), so a wave's four key groups reduce across its rows on the VALU
+        const int D4 = HD / 4;
+        constexpr int R = NT / 16;
+        const int rg = tid >> 4, d4 = min(tid & 15, D4 - 1);
         const f32x4* K4p = reinterpret_cast<const f32x4*>(ck + (int64_t)kvh * p.Smax * HD);
         const f32x4* V4p = reinterpret_cast<const f32x4*>(cv + (int64_t)kvh * p.Smax * HD);
-        const int qo = h * HD;
-        // only the K chunks past HD need zeroing (the q4 reads there land in k_new); a lane's
-        // score past pos is never kept and a V row past pos never used (P.V checks k < pos),
-        // so nothing else is masked — a select per element was ~100 VALU on this critical path
-        if (D4 < KPF) {  // uniform: none for HD = 4 KPF (stories15M)
-#pragma unroll
-            for (int i = 0; i < KPF; ++i)
-                if (i >= D4) kr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        const f32x4* q4 = reinterpret_cast<const f32x4*>(qs);
-        const f32x4* kn4 = reinterpret_cast<const f32x4*>(qs + HD);
-        const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
-        const int S = pos + 1;
-        // key tid from the prefetched row (rows past HD are zero: the q4 reads past HD land
-        // in the k / v part of qs and add nothing).  The new key's score (key pos, from k_new)
-        // is computed by every 16-lane group at once — chunk j of q . k_new, summed over the
-        // group — and selected by lane pos: loading k_new into that one lane's row was a
-        // divergent branch that held its wave (and the block_max barrier) back ~0.3 us
-        const int jn = min(tid & 15, D4 - 1);
-        const f32x4 qn = q4[jn], kn = kn4[jn];
-        float s_new = (tid & 15) < D4 ? qn.x * kn.x + qn.y * kn.y + qn.z * kn.z + qn.w * kn.w : 0.f;
-        s_new = group_sum<16>(s_new);
-        float s_own = 0.f;
-#pragma unroll
-        for (int i = 0; i < KPF; ++i) {
-            const f32x4 b = q4[i];
-            s_own += kr[i].x * b.x + kr[i].y * b.y + kr[i].z * b.z + kr[i].w * b.w;
-        }
-        s_own = tid == pos ? s_new : s_own;
-        float m = -INFINITY;
-        if (tid < S) {
-            sc[tid] = s_own;
-            m = s_own;
-        }
-        for (int k = tid + NT; k < S; k += NT) {
-            float s = 0.f;
-            // keys past the first NT (contexts longer than a workgroup; off the stories path):
-            // a plain loop — an unrolled row here held registers over the whole stage
-            for (int i = 0; i < D4; ++i) {
-                const f32x4 a = k == pos ? kn4[i] : K4p[(int64_t)k * D4 + i], b = q4[i];
-                s += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
-            }
-            sc[k] = s;
-            m = fmaxf(m, s);
-        }
-        if (li == 1) stamp(110);
-        m = block_max(c, m);
-        if (li == 1) stamp(111);
-        float l = 0.f;
-        for (int k = tid; k < S; k += NT) {
-            const float e = __builtin_amdgcn_exp2f(sc[k] - m);  // q carries log2(e) / sqrt(HD)
-            sc[k] = e;
-            l += e;
-        }
-        l = block_sum(c, l);  // its barrier also publishes sc
-        if (li == 1) stamp(112);
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        {
-            // every p read first (clamped index), then the FMAs with p zeroed past pos: a
-            // predicated read per key was a branch and an LDS wait per key
-            float pk[VPF];
-#pragma unroll
-            for (int t = 0; t < VPF; ++t) pk[t] = sc[min(rg + t * R, pos)];
-#pragma unroll
-            for (int t = 0; t < VPF; ++t) acc += (rg + t * R < pos ? pk[t] : 0.f) * vr[t];
-            for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
-            // the new key's row: every lane reads it, the key group owning it adds it (no
-            // divergent reads before the partials' barrier)
-            const float pn = sc[pos];
-            const f32x4 vn = vn4[d4];
-            acc += (pos % R == rg ? pn : 0.f) * vn;
-        }
-        if (li == 1) stamp(113);
-        // the four key groups of a wave summed across its 16-lane rows (permlane swaps), then
-        // the four waves' sums through LDS (a chain of 21 dependent adds over LDS partials
-        // was ~0.4 us)
-        {
-            auto rows = [](float v) {
-                const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-                v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
-                const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-                return __uint_as_float(b[0]) + __uint_as_float(b[1]);
-            };
-            acc = f32x4{rows(acc.x), rows(acc.y), rows(acc.z), rows(acc.w)};
-        }
-        f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
-        if ((tid & 63) < 16) part[(tid >> 6) * 16 + (tid & 15)] = acc;
-        lds_barrier();
-        if (li == 1) stamp(114);
-        if (tid < D4) {
-            f32x4 o = (part[tid] + part[16 + tid]) + (part[32 + tid] + part[48 + tid]);
-            o *= 1.0f / l;
-            gput(g_o + qo + 4 * tid + 0, tag, o.x);
-            gput(g_o + qo + 4 * tid + 1, tag, o.y);
-            gput(g_o + qo + 4 * tid + 2, tag, o.z);
-            gput(g_o + qo + 4 * tid + 3, tag, o.w);
-        }
-    };
-
-    if constexpr (FNP > 0) {
-        // ==== fold: head workgroup h computes its own q / k / v rows, no QKV hand-off ==========
-        // (the RMSNorm + QKV + RoPE of stage A and the attention of stage B in one workgroup; the
-        // other layer workgroups run stages C-E).  Its 3 HD rows of Wqkv (166 KB at stories15M)
-        // are more than its registers: the last FRP passes' rows (UPP each) go to registers, the
-        // rest to LDS by global_load_lds, both issued right after the previous layer's o is
-        // published: they land during the O-proj / FFN hand-offs, which the head workgroups sit
-        // out.  Layout (dynamic LDS, this role):
-        // [rows (pieces KB) | hin D | qs 3 HD | sc Smax + P.V partials | kvst n_layers x 4 HD | DMA sink 1 KB]
-        if (wg < H) {
-            const int h = wg, kvh = h / (H / KVH);
-            const int lane = tid & 63, wid = tid >> 6, un = tid / LPR, j = tid % LPR;
-            constexpr int FLP = FNP - FRP;        // passes from LDS
-            // KVL: every row in registers, and LDS holds this kv head's old K / V rows instead,
-            // DMA'd during the previous layer (loaded into registers after the dot they cost
-            // ~1 us of the CU's load rate on the path)
-            constexpr bool KVL = FLP == 0;
-            const int NRL = FLP * UPP;            // rows in LDS
-            const int rbytes = NRL * D * 4, SB = HD * D * 4;
-            const int npieces = fold_pieces(D, HD, FRP);
-            const int KVP = KVL ? (p.Smax * HD * 4 + 1023) / 1024 * 256 : 0;
-            float* rows = sm;
-            float* kvL = sm;  // KVL: [K rows | V rows] < pos of kv head kvh, KVP floats each
-            float* hinF = sm + (KVL ? 2 * KVP : npieces * 256);
-            float* qsF = hinF + p.Dp;
-            float* scF = qsF + ((3 * HD + 3) & ~3);
-            f32x4* kvst = reinterpret_cast<f32x4*>(scF + ((p.Smax + 3) & ~3) + 260);  // [layer][k new | v new | k old | v old]
-            float* scratch = reinterpret_cast<float*>(kvst + p.n_layers * HD);  // [256] DMA sink
-            // RoPE of this position (the same for every layer): pair tid of q (tid < HD / 2) or k
-            float2 cs = {1.f, 0.f};
-            if (tid < HD) {
-                const int t = pos * (HD >> 1) + (tid % (HD >> 1));
-                cs = float2{p.rope_cos[t], p.rope_sin[t]};
-            }
-            f32x4 kr[KPF], vr[VPF], wr[FRP][NCD], oldkv;
-            const int kvq = min(tid, 2 * D4 - 1);
-            // this layer's cache pointers, loaded with its rows (a scalar load of them after the
-            // QKV dot put ~1 us on the path: the scalar cache misses by then)
-            const float* ckl = nullptr;
-            const float* cvl = nullptr;
-            // layer li's loads, none of which depends on this step's values
-            auto issue = [&](int li) {
-                const char* wq = reinterpret_cast<const char*>(p.wqkv[li]);
-                const char* b0 = wq + (int64_t)h * SB;
-                const char* b1 = wq + (int64_t)(qdim + kvh * HD) * D * 4;
-                const char* b2 = wq + (int64_t)(qdim + kvdim + kvh * HD) * D * 4;
-                // opaque per call: the pieces' offsets are the same every layer, and hoisted out
-                // of the layer loop they held ~70 registers across it (spills)
-                int l16 = lane * 16;
-                asm volatile("" : "+v"(l16));
-#pragma unroll
-                for (int it = 0; it < FPW; ++it) {
-                    // piece pc: LDS bytes [1024 pc, +1024) = bytes of the head's rows [q | k | v];
-                    // pieces past the last re-copy it (same bytes, same place), the tail is clamped
-                    const int pc = min(wid + 4 * it, npieces - 1);
-                    const int b = min(pc * 1024 + l16, rbytes - 16);
-                    const int seg = (b >= SB) + (b >= 2 * SB);
-                    const char* src = (seg == 0 ? b0 : seg == 1 ? b1 : b2) + (b - seg * SB);
-                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                     (__attribute__((address_space(3))) void*)(rows + pc * 256), 16, 0, 0);
-                }
-                // the last FRP passes' rows (row (FLP + k) UPP + un of [q | k | v]) in registers
-                int row[FRP];
-#pragma unroll
-                for (int k = 0; k < FRP; ++k) {
-                    const int r = (FLP + k) * UPP + un, seg = r / HD, rr = r - seg * HD;
-                    row[k] = (seg == 0 ? h * HD : seg == 1 ? qdim + kvh * HD : qdim + kvdim + kvh * HD) + rr;
-                }
-                load_rows<FRP, NCD>(p.wqkv[li], row, K4d, wr);
-                // the old K / V rows of kv head kvh: KVL, into LDS; else into this XCD's L2
-                // (read for real after the QKV dot), register-free: LDS-DMA into one scratch
-                // piece, its contents unused
-                ckl = p.cache_k[li];
-                cvl = p.cache_v[li];
-                const int kvbytes = pos * HD * 4;
-                const char* kb = reinterpret_cast<const char*>(ckl + (int64_t)kvh * p.Smax * HD);
-                const char* vb = reinterpret_cast<const char*>(cvl + (int64_t)kvh * p.Smax * HD);
-                for (int pc = wid; pc * 1024 < kvbytes; pc += 4) {
-                    const int b = min(pc * 1024 + l16, kvbytes - 16);
-                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(kb + b),
-                                                     (__attribute__((address_space(3))) void*)(KVL ? kvL + pc * 256 : scratch), 16, 0, 0);
-                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(vb + b),
-                                                     (__attribute__((address_space(3))) void*)(KVL ? kvL + KVP + pc * 256 : scratch), 16, 0, 0);
-                }
-                if constexpr (KVL)
-                    oldkv = *gf4((kvq < D4 ? ckl : cvl) + ((int64_t)kvh * p.Smax + pos) * HD + 4 * (kvq % D4));
-            };
-            // the old K / V rows and the slots' previous contents (run-ahead undo: k for tid < D4,
-            // v for D4 <= tid < 2 D4), requested after the QKV dot: live across it (either of them)
-            // they left the dot's LDS reads no registers — each read waited for before the next
-            // (2.3 us for the dot)
-            // lane indices, opaque per layer: the K / V / score offsets derived from them are the
-            // same every layer, and hoisted out of the layer loop they held the registers the
-            // QKV dot's LDS reads need
-            int otid = tid;
-            auto issue_kv = [&](int li) {
-                load_kv(ckl, cvl, kvh, kr, vr, otid, otid >> 4, min(otid & 15, D4 - 1));
-                oldkv = *gf4((kvq < D4 ? ckl : cvl) + ((int64_t)kvh * p.Smax + pos) * HD + 4 * (kvq % D4));
-            };
-            // the token's embedding row (llama3.py:287) before layer 0's loads
-            const f32x4 e = gf4(p.emb + (int64_t)id * D)[min(tid, K4d - 1)];
-            issue(0);
-            for (int li = 0; li < p.n_layers; ++li) {
-                u64* g_qkv = p.gran + slab * li;
-                u64* g_o = g_qkv + qkvn;
-                otid = tid;
-                asm volatile("" : "+v"(otid));
-                if (li == 0) {
-                    if (tid < K4d) reinterpret_cast<f32x4*>(hinF)[tid] = e;
-                } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hinF, [](int i) { return i; })) {
-                    return;
-                }
-                // every wave's rows landed (its DMA counted in vmcnt), then visible to all waves
-                asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                stamp(1 + 10 * li);
-                // ---- RMSNorm + QKV (llama3.py:248, 166-168): row i * UPP + un of [q | k | v] ----
-                {
-                    f32x4 xv[NCD];
-                    read_x<NCD>(hinF, K4d, xv);
-                    const float rs = unit_inv_rms<NCD>(xv, D, p.eps);
-                    int rb = un * D;  // (opaque: see issue)
-                    asm volatile("" : "+v"(rb));
-                    // pass i: row i * UPP + un; the next row's LDS reads in flight during this
-                    // row's FMAs (two buffers), the 16-lane sums after every pass
-                    f32x4 w[2][NCD];
-                    auto rd = [&](int i, f32x4 (&b)[NCD]) {
-                        const f32x4* W4 = reinterpret_cast<const f32x4*>(rows + i * UPP * D + rb);
-#pragma unroll
-                        for (int t = 0; t < NCD; ++t) b[t] = W4[min(j + LPR * t, K4d - 1)];
-                    };
-                    auto dot = [&](const f32x4 (&b)[NCD]) {
-                        float a = 0.f;
-#pragma unroll
-                        for (int t = 0; t < NCD; ++t) a += b[t].x * xv[t].x + b[t].y * xv[t].y + b[t].z * xv[t].z + b[t].w * xv[t].w;
-                        return a;
-                    };
-                    float a[FNP];
-                    if constexpr (FLP > 0) rd(0, w[0]);
-#pragma unroll
-                    for (int i = 0; i < FNP; ++i) {
-                        if (i + 1 < FLP) rd(i + 1, w[(i + 1) & 1]);
-                        // (the scheduler otherwise issued one LDS read per wait)
-                        __builtin_amdgcn_sched_barrier(0);
-                        a[i] = i < FLP ? dot(w[i & 1]) : dot(wr[i - FLP]);
-                    }
-#pragma unroll
-                    for (int i = 0; i < FNP; ++i) a[i] = group_sum<LPR>(a[i]);
-                    if (j == 0) {
-#pragma unroll
-                        for (int i = 0; i < FNP; ++i) qsF[i * UPP + un] = a[i] * rs;
-                    }
-                }
-                if (li == 1) stamp(120);
-                if constexpr (KVL) {
-                    const f32x4* K4 = reinterpret_cast<const f32x4*>(kvL);
-                    const f32x4* V4 = reinterpret_cast<const f32x4*>(kvL + KVP);
-                    const int rgo = otid >> 4, d4o = min(otid & 15, D4 - 1);
-#pragma unroll
-                    for (int i = 0; i < KPF; ++i) kr[i] = K4[min(otid, kmax) * D4 + min(i, D4 - 1)];
-#pragma unroll
-                    for (int t = 0; t < VPF; ++t) vr[t] = V4[min(rgo + t * R, kmax) * D4 + d4o];
-                } else {
-                    issue_kv(li);
-                }
-                lds_barrier();
-                if (li == 1) stamp(121);
-                // ---- RoPE (llama3.py:169-181) on q (scaled) and k; the K / V rows and the slots'
-                // old contents kept for the end of the step ----------------------------------
-                f32x4* kv_l = kvst + li * HD;  // HD float4 per layer
-                if (tid < HD) {
-                    const int seg = tid >= (HD >> 1), i = tid - seg * (HD >> 1);
-                    float* x = qsF + seg * HD + 2 * i;
-                    const float v0 = x[0], v1 = x[1];
-                    const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
-                    const float s = seg ? 1.0f : p.q_scale;
-                    x[0] = r0 * s;
-                    x[1] = r1 * s;
-                    if (seg) reinterpret_cast<float2*>(kv_l)[i] = float2{r0, r1};
-                }
-                if (tid < D4) kv_l[D4 + tid] = reinterpret_cast<const f32x4*>(qsF + 2 * HD)[tid];
-                if (tid < 2 * D4) kv_l[2 * D4 + tid] = oldkv;
-                lds_barrier();
-                if (li == 1) stamp(122);
-                stamp(2 + 10 * li);
-                stamp(3 + 10 * li);
-                attend(li, h, ckl, cvl, qsF, scF, kr, vr, g_o, otid, otid >> 4, min(otid & 15, D4 - 1));
-                stamp(4 + 10 * li);
-                if (li + 1 < p.n_layers) {
-                    // (A/B knob) the next layer's 260 KB burst later, off the o hand-off
-                    if (p.fold_delay > 0) {
-                        const u64 t0 = __builtin_amdgcn_s_memrealtime();
-                        while (__builtin_amdgcn_s_memrealtime() - t0 < (u64)p.fold_delay) __builtin_amdgcn_s_sleep(4);
-                    }
-                    issue(li + 1);
-                }
-            }
-            // last wait: the last layer's output, i.e. every stage of every layer has published
-            // (workgroup 0: and every workgroup's start mark); then this kv head's K / V rows
-            {
-                u64* g_last = p.gran + slab * (p.n_layers - 1) + h2_off;
-                const int64_t mk = marks - g_last;
-                if (!sweep_n(c, g_last, wg == 0 ? D + G : D, hinF, [=](int i) { return i < D ? (int64_t)i : mk + (i - D); }, 8,
-                             false, 0))
-                    return;
-            }
-            if (h % (H / KVH) == 0 && tid < 2 * D4) {
-                const int sec = tid / D4, q = tid % D4;
-                const int64_t coff = ((int64_t)kvh * p.Smax + pos) * HD + 4 * q;
-                const int64_t boff = (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec) * KVH + kvh) * HD + 4 * q;
-                float* const* cache = sec ? p.cache_v : p.cache_k;
-                for (int li = 0; li < p.n_layers; ++li) {
-                    const f32x4* kv_l = kvst + li * HD;
-                    if (p.kv_bak) *reinterpret_cast<f32x4*>(p.kv_bak + (int64_t)li * p.bak_layer + boff) = kv_l[2 * D4 + tid];
-                    *reinterpret_cast<f32x4*>(cache[li] + coff) = kv_l[sec * D4 + q];
-                }
-            }
-        } else {
-            // ---- stages C-E on the layer workgroups past the heads ------------------------------
-            const int nwg = p.GL - H, wgc = wg - H;
-            for (int li = 0; li < p.n_layers; ++li) {
-                u64* g_qkv = p.gran + slab * li;
-                u64* g_o = g_qkv + qkvn;
-                u64* g_h1 = g_o + qdim;
-                u64* g_hid = g_h1 + D;
-                u64* g_h2 = g_hid + FD;
-                {  // O-proj + residual; the residual (the layer input) from the previous layer's output
-                    bool valid;
-                    const int u = stage_unit_of(D, wgc, nwg, valid);
-                    const int row[1] = {u};
-                    f32x4 w[1][NCD];
-                    load_rows<1, NCD>(p.wo[li], row, K4q, w);
-                    const int per = (D + nwg - 1) / nwg, u0 = wgc * per;
-                    float res = 0.f;
-                    if (li == 0) {
-                        res = p.emb[(int64_t)id * D + u];
-                        if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) return;
-                    } else {
-                        const int64_t hp = (p.gran + slab * (li - 1) + h2_off) - g_o;
-                        if (!sweep_n(c, g_o, qdim + per, xs, [=](int i) { return i < qdim ? (int64_t)i : hp + min(u0 + i - qdim, D - 1); }))
-                            return;
-                        res = xs[qdim + tid / LPR];
-                    }
-                    stamp(5 + 10 * li);
-                    float acc[1];
-                    dot_rows<1, NCD>(w, xs, K4q, acc);
-                    if (valid && tid % LPR == 0) gput(g_h1 + u, tag, res + acc[0]);
-                    stamp(6 + 10 * li);
-                }
-                {  // RMSNorm + gate|up + SwiGLU
-                    bool valid;
-                    const int u = stage_unit_of(FD, wgc, nwg, valid);
-                    int row[2];
-                    row[0] = 32 * (u / 16) + u % 16;
-                    row[1] = row[0] + 16;
-                    f32x4 w[2][NCD];
-                    load_rows<2, NCD>(p.wgu[li], row, K4d, w);
-                    if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) return;
-                    stamp(7 + 10 * li);
-                    float acc[2];
-                    const float rs = dot_rows_rms<2, NCD>(w, h1s, K4d, p.eps, acc);
-                    if (valid && tid % LPR == 0) {
-                        const float gt = acc[0] * rs, up = acc[1] * rs;
-                        gput(g_hid + u, tag, gt * __builtin_amdgcn_rcpf(1.0f + __expf(-gt)) * up);
-                    }
-                    stamp(8 + 10 * li);
-                }
-                {  // down + residual
-                    bool valid;
-                    const int u = stage_unit_of(D, wgc, nwg, valid);
-                    const int row[1] = {u};
-                    f32x4 w[1][NCF];
-                    load_rows<1, NCF>(p.wd[li], row, K4f, w);
-                    if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) return;
-                    stamp(9 + 10 * li);
-                    float acc[1];
-                    dot_rows<1, NCF>(w, xs, K4f, acc);
-                    if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);
-                    stamp(10 + 10 * li);
-                }
-            }
-            return;  // no K / V rows here; workgroup 0 is a head workgroup
-        }
-    } else {
-        for (int li = 0; li < p.n_layers; ++li) {
-            u64* g_qkv = p.gran + slab * li;
-            u64* g_o = g_qkv + qkvn;
-            u64* g_h1 = g_o + qdim;
-            u64* g_hid = g_h1 + D;
-            u64* g_h2 = g_hid + FD;
-            const float* wqkv = p.wqkv[li];
-            const float* ck = p.cache_k[li];
-            const float* cv = p.cache_v[li];
-            // the attention workgroup's K / V rows of this layer, fetched in stage B before its
-            // hand-off wait (fetched at the layer's start instead, ahead of the QKV rows, the step
-            // measured 0.091 against 0.087 ms)
-            const int kvh = wg / (H / KVH);
-            f32x4 kr[KPF], vr[VPF];
-            // ---- stage A: RMSNorm + QKV + RoPE (llama3.py:248, 166-181); the K / V append
-            // (:184-185) waits for the end of the step (see the header) ------------------------
-            {
-                bool valid;
-                const int u = stage_unit(p, qkvn / 2, wg, valid);  // RoPE pair (rows 2u, 2u + 1)
-                const int row[2] = {2 * u, 2 * u + 1};
-                f32x4 w[2][NCD];
-                load_rows<2, NCD>(wqkv, row, K4d, w);
-                const int col = 2 * u;
-                const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
-                const int cc = col - (sec == 0 ? 0 : sec == 1 ? qdim : qdim + kvdim);
-                const int head = cc / HD, d = cc - head * HD;
-                float2 cs = {1.f, 0.f};
-                if (sec < 2) {
-                    const int t = pos * (HD >> 1) + (d >> 1);
-                    cs = float2{p.rope_cos[t], p.rope_sin[t]};
-                }
-                // the slot's previous contents, for the run-ahead undo (kv_bak, written at the end)
-                float2 old = {0.f, 0.f};
-                if (p.kv_bak && sec > 0 && valid)
-                    old = *reinterpret_cast<const float2*>((sec == 1 ? ck : cv) + ((int64_t)head * p.Smax + pos) * HD + d);
-                // the layer input: the token's embedding row (llama3.py:287), else the previous
-                // layer's output granules
-                if (li == 0) {
-                    // one float4 per thread, one round trip (D / 4 <= NT by eligibility; a float
-                    // per thread took two dependent trips for D > NT)
-                    const gf4p E4 = gf4(p.emb + (int64_t)id * D);
-                    const f32x4 e = E4[min(tid, K4d - 1)];
-                    if (tid < K4d) reinterpret_cast<f32x4*>(hin)[tid] = e;
-                    lds_barrier();
-                } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
-                    return;
-                }
-                stamp(1 + 10 * li);
-                float acc[2];
-                const float rs = dot_rows_rms<2, NCD>(w, hin, K4d, p.eps, acc);
-                if (valid && tid % LPR == 0) {
-                    const float v0 = acc[0] * rs, v1 = acc[1] * rs;
-                    const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
-                    const float s = sec == 0 ? p.q_scale : 1.0f;
-                    gput(g_qkv + col, tag, r0 * s);
-                    gput(g_qkv + col + 1, tag, r1 * s);
-                    if (sec > 0) kvs[li * UPP + tid / LPR] = f32x4{r0, r1, old.x, old.y};
-                }
-                stamp(2 + 10 * li);
-            }
-            // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ----------
-            if (wg < H) {
-                const int qo = wg * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
-                load_kv(ck, cv, kvh, kr, vr, tid, rg, d4);
-                if (!sweep_n(c, g_qkv, 3 * HD, xs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
-                    return;
-                stamp(3 + 10 * li);
-                attend(li, wg, ck, cv, xs, sc, kr, vr, g_o, tid, rg, d4);
-                stamp(4 + 10 * li);
-            }
-            // ---- stage C: O-proj + residual (llama3.py:211, 253) ------------------------------
-            {
-                bool valid;
-                const int u = stage_unit(p, D, wg, valid);
-                const int row[1] = {u};
-                f32x4 w[1][NCD];
-                load_rows<1, NCD>(p.wo[li], row, K4q, w);
-                if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) return;
-                stamp(5 + 10 * li);
-                float acc[1];
-                dot_rows<1, NCD>(w, xs, K4q, acc);
-                if (valid && tid % LPR == 0) gput(g_h1 + u, tag, hin[u] + acc[0]);
-                stamp(6 + 10 * li);
-            }
-            // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) ---------------------
-            {
-                bool valid;
-                // unit u: hidden unit u, fused rows 32(u/16) + u%16 (gate) and +16 (up)
-                const int u = stage_unit(p, FD, wg, valid);
-                int row[2];
-                row[0] = 32 * (u / 16) + u % 16;
-                row[1] = row[0] + 16;
-                f32x4 w[2][NCD];
-                load_rows<2, NCD>(p.wgu[li], row, K4d, w);
-                if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) return;
-                stamp(7 + 10 * li);
-                float acc[2];
-                const float rs = dot_rows_rms<2, NCD>(w, h1s, K4d, p.eps, acc);
-                if (valid && tid % LPR == 0) {
-                    const float gt = acc[0] * rs, up = acc[1] * rs;
-                    gput(g_hid + u, tag, gt * __builtin_amdgcn_rcpf(1.0f + __expf(-gt)) * up);
-                }
-                stamp(8 + 10 * li);
-            }
-            // ---- stage E: down + residual (llama3.py:102, 259) ----------------------------------
-            {
-                bool valid;
-                const int u = stage_unit(p, D, wg, valid);
-                const int row[1] = {u};
-                f32x4 w[1][NCF];
-                load_rows<1, NCF>(p.wd[li], row, K4f, w);
-                // workgroup 0's last wait also covers every workgroup's start mark (they were
-                // written at launch: no extra round trip for the check the epoch bump needs)
-                const bool last0 = wg == 0 && li + 1 == p.n_layers;
-                const int64_t mk = marks - g_hid;
-                if (!sweep_n(c, g_hid, last0 ? FD + G : FD, xs, [=](int i) { return i < FD ? (int64_t)i : mk + (i - FD); }, 1,
-                             false, FD))
-                    return;
-                stamp(9 + 10 * li);
-                float acc[1];
-                dot_rows<1, NCF>(w, xs, K4f, acc);
-                if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);  // the last layer's: to the lm workgroups
-                stamp(10 + 10 * li);
-            }
-        }
-        // ---- every layer workgroup past its last wait: every stage of every layer has published --
-        // the step's K / V rows into the caches (llama3.py:184-185), each slot's previous contents
-        // into kv_bak [pos % KV_BAK_SLOTS][k, v][1][KVH][HD] (the run-ahead undo, GemmArgs::kv_bak):
-        // stores only, from LDS (the next launch reads the rows with plain loads after the kernel
-        // boundary)
+        constexpr int VPF = NT / R;  // V rows per lane: the first NT keys
+        // unpredicated loads from clamped rows (see load_rows), zeroed where used; row pos - 1 is
+        // the last one an earlier launch wrote (pos >= 1 in a decode step)
+        const int kmax = pos > 0 ? pos - 1 : 0;
+        const gf4p Kg = gf4(K4p), Vg = gf4(V4p);
+        f32x4 kr[KPF], vr[VPF];
+        // ---- stage A: RMSNorm + QKV + RoPE (llama3.py:248, 166-181); the K / V append
+        // (:184-185) waits for the end of the step (see the header) ----------------------------
         {
             bool valid;
-            const int u = stage_unit(p, qkvn / 2, wg, valid);
+            const int u = stage_unit(p, qkvn / 2, wg, valid);  // RoPE pair (rows 2u, 2u + 1)
+            const int row[2] = {2 * u, 2 * u + 1};
+            f32x4 w[2][NCD];
+            load_rows<2, NCD>(wqkv, row, K4d, w);
             const int col = 2 * u;
             const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
-            if (valid && sec > 0 && tid % LPR == 0) {
-                const int cc = col - (sec == 1 ? qdim : qdim + kvdim);
-                const int head = cc / HD, d = cc - head * HD;
-                const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
-                const int64_t boff = (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d;
-                float* const* cache = sec == 1 ? p.cache_k : p.cache_v;
-                for (int li = 0; li < p.n_layers; ++li) {
-                    const f32x4 e = kvs[li * UPP + tid / LPR];
-                    if (p.kv_bak) *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer + boff) = float2{e.z, e.w};
-                    *reinterpret_cast<float2*>(cache[li] + coff) = float2{e.x, e.y};
+            const int cc = col - (sec == 0 ? 0 : sec == 1 ? qdim : qdim + kvdim);
+            const int head = cc / HD, d = cc - head * HD;
+            float2 cs = {1.f, 0.f};
+            if (sec < 2) {
+                const int t = pos * (HD >> 1) + (d >> 1);
+                cs = float2{p.rope_cos[t], p.rope_sin[t]};
+            }
+            // the slot's previous contents, for the run-ahead undo (kv_bak, written at the end)
+            float2 old = {0.f, 0.f};
+            if (p.kv_bak && sec > 0 && valid)
+                old = *reinterpret_cast<const float2*>((sec == 1 ? ck : cv) + ((int64_t)head * p.Smax + pos) * HD + d);
+            // the layer input: the token's embedding row (llama3.py:287), else the previous
+            // layer's output granules
+            if (li == 0) {
+                // one float4 per thread, one round trip (D / 4 <= NT by eligibility; a float per
+                // thread took two dependent trips for D > NT)
+                const gf4p E4 = gf4(p.emb + (int64_t)id * D);
+                const f32x4 e = E4[min(tid, K4d - 1)];
+                if (tid < K4d) reinterpret_cast<f32x4*>(hin)[tid] = e;
+                lds_barrier();
+            } else if (!sweep_n(c, p.gran + slab * (li - 1) + h2_off, D, hin, [](int i) { return i; })) {
+                return;
+            }
+            stamp(1 + 10 * li);
+            float acc[2];
+            const float rs = dot_rows_rms<2, NCD>(w, hin, K4d, p.eps, acc);
+            if (valid && tid % LPR == 0) {
+                const float v0 = acc[0] * rs, v1 = acc[1] * rs;
+                const float r0 = v0 * cs.x - v1 * cs.y, r1 = v0 * cs.y + v1 * cs.x;
+                const float s = sec == 0 ? p.q_scale : 1.0f;
+                gput(g_qkv + col, tag, r0 * s);
+                gput(g_qkv + col + 1, tag, r1 * s);
+                if (sec > 0) kvs[li * UPP + tid / LPR] = f32x4{r0, r1, old.x, old.y};
+            }
+            stamp(2 + 10 * li);
+        }
+        // ---- stage B: attention of head wg (llama3.py:186-210), the others go on ------------
+        if (wg < H) {
+            const int h = wg;
+            float* qs = xs;                              // q | k_new | v_new of this head
+            const int qo = h * HD, ko = qdim + kvh * HD, vo = qdim + kvdim + kvh * HD;
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) kr[i] = Kg[(int64_t)min(tid, kmax) * D4 + min(i, D4 - 1)];
+#pragma unroll
+            for (int t = 0; t < VPF; ++t) vr[t] = Vg[(int64_t)min(rg + t * R, kmax) * D4 + d4];
+            if (!sweep_n(c, g_qkv, 3 * HD, qs, [=](int i) { return i < HD ? qo + i : i < 2 * HD ? ko + i - HD : vo + i - 2 * HD; }))
+                return;
+            stamp(3 + 10 * li);
+            // only the K chunks past HD need zeroing (the q4 reads there land in k_new); a lane's
+            // score past pos is never kept and a V row past pos never used (P.V checks k < pos),
+            // so nothing else is masked — a select per element was ~100 VALU on this critical path
+            if (D4 < KPF) {  // uniform: none for HD = 4 KPF (stories15M)
+#pragma unroll
+                for (int i = 0; i < KPF; ++i)
+                    if (i >= D4) kr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            const f32x4* q4 = reinterpret_cast<const f32x4*>(qs);
+            const f32x4* kn4 = reinterpret_cast<const f32x4*>(qs + HD);
+            const f32x4* vn4 = reinterpret_cast<const f32x4*>(qs + 2 * HD);
+            const int S = pos + 1;
+            // key tid from the prefetched row (rows past HD are zero: the q4 reads past HD land
+            // in the k / v part of qs and add nothing).  The new key's score (key pos, from k_new)
+            // is computed by every 16-lane group at once — chunk j of q . k_new, summed over the
+            // group — and selected by lane pos: loading k_new into that one lane's row was a
+            // divergent branch that held its wave (and the block_max barrier) back ~0.3 us
+            const int jn = min(tid & 15, D4 - 1);
+            const f32x4 qn = q4[jn], kn = kn4[jn];
+            float s_new = (tid & 15) < D4 ? qn.x * kn.x + qn.y * kn.y + qn.z * kn.z + qn.w * kn.w : 0.f;
+            s_new = group_sum<16>(s_new);
+            float s_own = 0.f;
+#pragma unroll
+            for (int i = 0; i < KPF; ++i) {
+                const f32x4 b = q4[i];
+                s_own += kr[i].x * b.x + kr[i].y * b.y + kr[i].z * b.z + kr[i].w * b.w;
+            }
+            s_own = tid == pos ? s_new : s_own;
+            float m = -INFINITY;
+            if (tid < S) {
+                sc[tid] = s_own;
+                m = s_own;
+            }
+            for (int k = tid + NT; k < S; k += NT) {
+                float s = 0.f;
+                // keys past the first NT (contexts longer than a workgroup; off the stories path):
+                // a plain loop — an unrolled row here held registers over the whole stage
+                for (int i = 0; i < D4; ++i) {
+                    const f32x4 a = k == pos ? kn4[i] : K4p[(int64_t)k * D4 + i], b = q4[i];
+                    s += a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
                 }
+                sc[k] = s;
+                m = fmaxf(m, s);
+            }
+            if (li == 1) stamp(110);
+            m = block_max(c, m);
+            if (li == 1) stamp(111);
+            float l = 0.f;
+            for (int k = tid; k < S; k += NT) {
+                const float e = __builtin_amdgcn_exp2f(sc[k] - m);  // q carries log2(e) / sqrt(HD)
+                sc[k] = e;
+                l += e;
+            }
+            l = block_sum(c, l);  // its barrier also publishes sc
+            if (li == 1) stamp(112);
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            {
+                // every p read first (clamped index), then the FMAs with p zeroed past pos: a
+                // predicated read per key was a branch and an LDS wait per key
+                float pk[VPF];
+#pragma unroll
+                for (int t = 0; t < VPF; ++t) pk[t] = sc[min(rg + t * R, pos)];
+#pragma unroll
+                for (int t = 0; t < VPF; ++t) acc += (rg + t * R < pos ? pk[t] : 0.f) * vr[t];
+                for (int k = rg + VPF * R; k < pos; k += R) acc += sc[k] * V4p[(int64_t)k * D4 + d4];
+                // the new key's row: every lane reads it, the key group owning it adds it (no
+                // divergent reads before the partials' barrier)
+                const float pn = sc[pos];
+                const f32x4 vn = vn4[d4];
+                acc += (pos % R == rg ? pn : 0.f) * vn;
+            }
+            if (li == 1) stamp(113);
+            // the four key groups of a wave summed across its 16-lane rows (permlane swaps), then
+            // the four waves' sums through LDS (a chain of 21 dependent adds over LDS partials
+            // was ~0.4 us)
+            {
+                auto rows = [](float v) {
+                    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                    v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+                    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+                    return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+                };
+                acc = f32x4{rows(acc.x), rows(acc.y), rows(acc.z), rows(acc.w)};
+            }
+            f32x4* part = reinterpret_cast<f32x4*>(sc + ((S + 3) & ~3));
+            if ((tid & 63) < 16) part[(tid >> 6) * 16 + (tid & 15)] = acc;
+            lds_barrier();
+            if (li == 1) stamp(114);
+            if (tid < D4) {
+                f32x4 o = (part[tid] + part[16 + tid]) + (part[32 + tid] + part[48 + tid]);
+                o *= 1.0f / l;
+                gput(g_o + qo + 4 * tid + 0, tag, o.x);
+                gput(g_o + qo + 4 * tid + 1, tag, o.y);
+                gput(g_o + qo + 4 * tid + 2, tag, o.z);
+                gput(g_o + qo + 4 * tid + 3, tag, o.w);
+            }
+            stamp(4 + 10 * li);
+        }
+        // ---- stage C: O-proj + residual (llama3.py:211, 253) --------------------------------
+        {
+            bool valid;
+            const int u = stage_unit(p, D, wg, valid);
+            const int row[1] = {u};
+            f32x4 w[1][NCD];
+            load_rows<1, NCD>(p.wo[li], row, K4q, w);
+            if (!sweep_n(c, g_o, qdim, xs, [](int i) { return i; })) return;
+            stamp(5 + 10 * li);
+            float acc[1];
+            dot_rows<1, NCD>(w, xs, K4q, acc);
+            if (valid && tid % LPR == 0) gput(g_h1 + u, tag, hin[u] + acc[0]);
+            stamp(6 + 10 * li);
+        }
+        // ---- stage D: RMSNorm + gate|up + SwiGLU (llama3.py:256, 97-101) -----------------------
+        {
+            bool valid;
+            // unit u: hidden unit u, fused rows 32(u/16) + u%16 (gate) and +16 (up)
+            const int u = stage_unit(p, FD, wg, valid);
+            int row[2];
+            row[0] = 32 * (u / 16) + u % 16;
+            row[1] = row[0] + 16;
+            f32x4 w[2][NCD];
+            load_rows<2, NCD>(p.wgu[li], row, K4d, w);
+            if (!sweep_n(c, g_h1, D, h1s, [](int i) { return i; })) return;
+            stamp(7 + 10 * li);
+            float acc[2];
+            const float rs = dot_rows_rms<2, NCD>(w, h1s, K4d, p.eps, acc);
+            if (valid && tid % LPR == 0) {
+                const float gt = acc[0] * rs, up = acc[1] * rs;
+                gput(g_hid + u, tag, gt * __builtin_amdgcn_rcpf(1.0f + __expf(-gt)) * up);
+            }
+            stamp(8 + 10 * li);
+        }
+        // ---- stage E: down + residual (llama3.py:102, 259) ------------------------------------
+        {
+            bool valid;
+            const int u = stage_unit(p, D, wg, valid);
+            const int row[1] = {u};
+            f32x4 w[1][NCF];
+            load_rows<1, NCF>(p.wd[li], row, K4f, w);
+            // workgroup 0's last wait also covers every workgroup's start mark (they were written
+            // at launch: no extra round trip for the check the epoch bump needs)
+            const bool last0 = wg == 0 && li + 1 == p.n_layers;
+            const int64_t mk = marks - g_hid;
+            if (!sweep_n(c, g_hid, last0 ? FD + G : FD, xs, [=](int i) { return i < FD ? (int64_t)i : mk + (i - FD); }, 1,
+                         false, FD))
+                return;
+            stamp(9 + 10 * li);
+            float acc[1];
+            dot_rows<1, NCF>(w, xs, K4f, acc);
+            if (valid && tid % LPR == 0) gput(g_h2 + u, tag, h1s[u] + acc[0]);  // the last layer's: to the lm workgroups
+            stamp(10 + 10 * li);
+        }
+    }
+    // ---- every layer workgroup past its last wait: every stage of every layer has published ----
+    // the step's K / V rows into the caches (llama3.py:184-185), each slot's previous contents into
+    // kv_bak [pos % KV_BAK_SLOTS][k, v][1][KVH][HD] (the run-ahead undo, GemmArgs::kv_bak): stores
+    // only, from LDS (the next launch reads the rows with plain loads after the kernel boundary)
+    {
+        bool valid;
+        const int u = stage_unit(p, qkvn / 2, wg, valid);
+        const int col = 2 * u;
+        const int sec = col < qdim ? 0 : col < qdim + kvdim ? 1 : 2;
+        if (valid && sec > 0 && tid % LPR == 0) {
+            const int cc = col - (sec == 1 ? qdim : qdim + kvdim);
+            const int head = cc / HD, d = cc - head * HD;
+            const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
+            const int64_t boff = (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d;
+            float* const* cache = sec == 1 ? p.cache_k : p.cache_v;
+            for (int li = 0; li < p.n_layers; ++li) {
+                const f32x4 e = kvs[li * UPP + tid / LPR];
+                if (p.kv_bak) *reinterpret_cast<float2*>(p.kv_bak + (int64_t)li * p.bak_layer + boff) = float2{e.z, e.w};
+                *reinterpret_cast<float2*>(cache[li] + coff) = float2{e.x, e.y};
             }
         }
     }
@@ -1057,49 +743,38 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     }
 }
 
-// Instances (chunk counts rounded up; the loads past K are clamped): X(NCD, NCF, KPF, LMPF, FNP,
-// FRP, FPW) — FNP > 0: the fold layout (3 HD = 16 FNP; FRP of the passes from registers; FPW: LDS
-// pieces per wave, >= fold_pieces / 4)
-#define L3_PERSIST_INSTANCES(X)                                                                    \
-    X(1, 3, 16, 8, 0, 0, 0)     /* tiny models (tests) */                                             \
-    X(5, 12, 12, 11, 0, 0, 0)   /* stories15M: D 288, FD 768, HD 48 (167 lm rows per lm workgroup) */ \
-    X(5, 12, 12, 11, 9, 5, 18)  /* stories15M, fold 1: 64 of the head's 144 rows in LDS (72 pieces) */ \
-    X(5, 12, 12, 11, 9, 9, 0)   /* stories15M, fold 2: every row in registers, old K / V in LDS */ \
-    X(5, 12, 16, 8, 0, 0, 0)    /* the same D / FD with HD 52..64 (D 256: 4 heads of 64) */           \
-    X(5, 16, 16, 4, 0, 0, 0)                                                                          \
-    X(8, 16, 16, 2, 0, 0, 0)                                                                          \
-    X(1, 12, 16, 8, 0, 0, 0)                                                                          \
-    X(5, 3, 16, 8, 0, 0, 0)                                                                           \
-    X(8, 12, 16, 2, 0, 0, 0)
+// Instances (chunk counts rounded up; the loads past K are clamped): X(NCD, NCF, KPF, LMPF)
+#define L3_PERSIST_INSTANCES(X)                                                                   \
+    X(1, 3, 16, 8)    /* tiny models (tests) */                                                   \
+    X(5, 12, 12, 11)  /* stories15M: D 288, FD 768, HD 48 (167 lm rows per lm workgroup) */       \
+    X(5, 12, 16, 8)   /* the same D / FD with HD 52..64 (D 256: 4 heads of 64) */                 \
+    X(5, 16, 16, 4)                                                                               \
+    X(8, 16, 16, 2)                                                                               \
+    X(1, 12, 16, 8)                                                                               \
+    X(5, 3, 16, 8)                                                                                \
+    X(8, 12, 16, 2)
 
 static int ncd_of(int D) { const int n = (D + 63) / 64; return n <= 1 ? 1 : n <= 5 ? 5 : n <= 8 ? 8 : 0; }
 static int ncf_of(int FD) { const int n = (FD + 63) / 64; return n <= 3 ? 3 : n <= 12 ? 12 : n <= 16 ? 16 : 0; }
 
 // the first instance that takes the shape: its (D, FD) chunking and KPF >= HD / 4 (a KPF short of
-// HD / 4 would drop the old keys' last dims from their scores); with a.fold, a fold instance whose
-// passes are the head's rows and whose pieces cover them
-struct PersistInstance { int ncd, ncf, kpf, lmpf, fnp, frp, fpw; };
+// HD / 4 would drop the old keys' last dims from their scores)
+struct PersistInstance { int ncd, ncf, kpf, lmpf; };
 static const PersistInstance kPersistInstances[] = {
-#define L3_ROW(A, B, C, E, F, R, W) {A, B, C, E, F, R, W},
+#define L3_ROW(A, B, C, E) {A, B, C, E},
     L3_PERSIST_INSTANCES(L3_ROW)
 #undef L3_ROW
 };
 static const PersistInstance* persist_instance(const DecodePersistArgs& a) {
     const int ncd = ncd_of(a.D), ncf = ncf_of(a.FD);
-    for (const PersistInstance& x : kPersistInstances) {
-        if (x.ncd != ncd || x.ncf != ncf || a.HD / 4 > x.kpf || (x.fnp > 0) != (a.fold != 0)) continue;
-        if (x.fnp > 0 && (16 * x.fnp != 3 * a.HD || persist::fold_pieces(a.D, a.HD, x.frp) > 4 * x.fpw ||
-                          (a.fold == 2) != (x.frp == x.fnp)))
-            continue;
-        return &x;
-    }
+    for (const PersistInstance& x : kPersistInstances)
+        if (x.ncd == ncd && x.ncf == ncf && a.HD / 4 <= x.kpf) return &x;
     return nullptr;
 }
 
 static const void* persist_kernel(const PersistInstance* x) {
-#define L3_FN(A, B, C, E, F, R, W)                                                                           \
-    if (x->ncd == A && x->ncf == B && x->kpf == C && x->lmpf == E && x->fnp == F && x->frp == R && x->fpw == W) \
-        return reinterpret_cast<const void*>(&decode_persist_kernel<A, B, C, E, F, R, W>);
+#define L3_FN(A, B, C, E) \
+    if (x->ncd == A && x->ncf == B && x->kpf == C && x->lmpf == E) return reinterpret_cast<const void*>(&decode_persist_kernel<A, B, C, E>);
     L3_PERSIST_INSTANCES(L3_FN)
 #undef L3_FN
     return nullptr;
@@ -1107,29 +782,15 @@ static const void* persist_kernel(const PersistInstance* x) {
 
 bool decode_persist_ok(const DecodePersistArgs& a) {
     const int qkvn = (a.H + 2 * a.KVH) * a.HD;
-    const bool base = a.D % 4 == 0 && a.FD % 4 == 0 && a.HD % 4 == 0 && a.HD >= 4 && a.HD <= 64 && a.H <= a.GL &&
-                      a.H % a.KVH == 0 && a.H * a.HD == a.D && persist_instance(a) && qkvn % 2 == 0 &&
-                      (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD + a.GL - 1) / a.GL <= persist::UPP &&
-                      (a.D + a.GL - 1) / a.GL <= persist::UPP && a.D / 4 <= persist::NT && a.Smax >= 1 &&
-                      a.Smax <= 8192 && a.VS >= 1 && a.n_layers >= 1 && a.GL >= 1 && a.GL < 256;
-    if (!base || !a.fold) return base;
-    // fold: the head's last UPP rows are v rows (HD >= 16); stages C-E on the GL - H others, the
-    // O-proj's wait also carries its units' residual granules
-    const int nwg = a.GL - a.H;
-    return a.HD >= 16 && nwg >= 1 && (a.D + nwg - 1) / nwg <= persist::UPP && (a.FD + nwg - 1) / nwg <= persist::UPP &&
-           a.H * a.HD + (a.D + nwg - 1) / nwg <= 5 * persist::NT;
+    return a.D % 4 == 0 && a.FD % 4 == 0 && a.HD % 4 == 0 && a.HD >= 4 && a.HD <= 64 && a.H <= a.GL &&
+           a.H % a.KVH == 0 && a.H * a.HD == a.D && persist_instance(a) && qkvn % 2 == 0 &&
+           (qkvn / 2 + a.GL - 1) / a.GL <= persist::UPP && (a.FD + a.GL - 1) / a.GL <= persist::UPP &&
+           (a.D + a.GL - 1) / a.GL <= persist::UPP && a.D / 4 <= persist::NT && a.Smax >= 1 && a.Smax <= 8192 && a.VS >= 1 &&
+           a.n_layers >= 1 && a.GL >= 1 && a.GL < 256;
 }
 
-// dynamic LDS: K / V pairs, hin, h1s, xs, scores, P.V partials; fold: the head workgroups' layout
-// (decode_persist_kernel) when larger
-static size_t persist_lds(const DecodePersistArgs& a) {
-    const size_t base = ((size_t)4 * persist::UPP * a.n_layers + 2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
-    if (!a.fold) return base;
-    const PersistInstance* x = persist_instance(a);
-    const size_t lead = x->frp == x->fnp ? (size_t)2 * ((a.Smax * a.HD * 4 + 1023) / 1024 * 256)  // old K / V rows
-                                         : (size_t)persist::fold_pieces(a.D, a.HD, x->frp) * 256;  // Wqkv rows
-    const size_t fold = (lead + a.Dp + ((3 * a.HD + 3) & ~3) + ((a.Smax + 3) & ~3) + 260 + (size_t)4 * a.HD * a.n_layers + 256) * 4;
-    return fold > base ? fold : base;
+static size_t persist_lds(const DecodePersistArgs& a) {  // K / V pairs, hin, h1s, xs, scores, P.V partials
+    return ((size_t)4 * persist::UPP * a.n_layers + 2 * a.Dp + a.Xp + a.Smax + 4 + 256 * 4 + 64) * 4;
 }
 
 // Grid of one decode step, 0 when the step cannot run on this device: one workgroup per CU (256
@@ -1137,28 +798,23 @@ static size_t persist_lds(const DecodePersistArgs& a) {
 // grid must not exceed the CUs times the blocks per CU the kernel's resources admit (its
 // registers hold it to 1; checked with the occupancy query at the dynamic LDS).  Fewer CUs than
 // the layer workgroups + the lm workgroups need (a CPX partition's 32) means no persistent step.
-// L3_DECODE_PERSIST_MAX_CUS caps the CU count seen (test knob).  Past 64 KB of dynamic LDS (the
-// fold) the kernel's cap is raised here, before any capture.
+// L3_DECODE_PERSIST_MAX_CUS caps the CU count seen (test knob).
 int decode_persist_grid(const DecodePersistArgs& a) {
     if (!decode_persist_ok(a)) return 0;
-    int dev = 0, cus = 0, lds_cu = 0;
+    int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess)
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return 0;
     const int cap = env_knob("L3_DECODE_PERSIST_MAX_CUS", 0);
     if (cap > 0 && cap < cus) cus = cap;
     const int grid = cus < 256 ? cus : 256;
     if (grid <= a.GL || 2 * (grid - a.GL) > a.Xp) return 0;
     const size_t lds = persist_lds(a);
-    const void* fn = persist_kernel(persist_instance(a));
-    hipFuncAttributes fa{};
-    if (!fn || hipFuncGetAttributes(&fa, fn) != hipSuccess || lds + fa.sharedSizeBytes > (size_t)lds_cu) return 0;
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return 0;
+    if (lds > 64 * 1024) return 0;  // (the default dynamic LDS cap)
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu < 1) return 0;
+    const void* fn = persist_kernel(persist_instance(a));
+    if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, lds) != hipSuccess || per_cu < 1)
+        return 0;
     return grid;
 }
 
@@ -1166,9 +822,9 @@ hipError_t launch_decode_persist(const DecodePersistArgs& a, int grid, hipStream
     if (grid < 1 || grid > 256 || grid <= a.GL || !decode_persist_ok(a)) return hipErrorNotSupported;
     const size_t lds = persist_lds(a);
     const PersistInstance* x = persist_instance(a);
-#define L3_LAUNCH(A, B, C, E, F, R, W)                                                                         \
-    if (x->ncd == A && x->ncf == B && x->kpf == C && x->lmpf == E && x->fnp == F && x->frp == R && x->fpw == W) { \
-        hipLaunchKernelGGL((decode_persist_kernel<A, B, C, E, F, R, W>), dim3(grid), dim3(256), lds, s, a);    \
+#define L3_LAUNCH(A, B, C, E)                                                                            \
+    if (x->ncd == A && x->ncf == B && x->kpf == C && x->lmpf == E) {                                     \
+        hipLaunchKernelGGL((decode_persist_kernel<A, B, C, E>), dim3(grid), dim3(256), lds, s, a);      \
         return hipGetLastError();                                                                        \
     }
     L3_PERSIST_INSTANCES(L3_LAUNCH)

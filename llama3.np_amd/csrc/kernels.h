@@ -288,11 +288,6 @@ struct DecodePersistArgs {
     unsigned* err;                 // host-mapped: pos + 1 of the step in which a workgroup gave up
     unsigned long long* stamps;    // diagnostic (null): [workgroup][128] s_memrealtime at stage points
     int fault_pos, fault_wg;       // test knob: workgroup fault_wg gives up in the step at fault_pos (-1: none)
-    int lm_delay, lm_gap;          // ticks (100 MHz) the lm workgroups wait before requesting their rows,
-                                   // and between their passes
-    int fold_delay;                // ticks the fold's head workgroups wait before the next layer's loads
-    int fold;                      // 1: head workgroups compute their own q / k / v rows (no QKV hand-off;
-                                   //    decode_persist.hip "fold"), 0: the QKV stage over every layer workgroup
 };
 // granules per layer of the persistent step: [qkv | o | h1 | hid | h2]
 __host__ __device__ inline int64_t decode_persist_slab(int H, int KVH, int HD, int D, int FD) {

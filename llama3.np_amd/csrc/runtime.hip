@@ -1020,12 +1020,6 @@ static DecodePersistArgs persist_shape(const l3_ctx* c) {
     if (xp < 512) xp = 512;  // the final argmax's 2 x 256 partials
     a.Xp = (xp + 3) & ~3;
     a.fault_pos = -1;
-    // the fold layout (L3_DECODE_PERSIST_FOLD) where the shape has an instance for it
-    a.fold = env_knob("L3_DECODE_PERSIST_FOLD", 0);  // 1, 2: the two fold instances (decode_persist.hip)
-    a.lm_delay = env_knob("L3_DECODE_PERSIST_LM_DELAY", 0);  // (A/B knobs, decode_persist.hip)
-    a.fold_delay = env_knob("L3_DECODE_PERSIST_FOLD_DELAY", 0);
-    a.lm_gap = env_knob("L3_DECODE_PERSIST_LM_GAP", 0);
-    if (a.fold && !decode_persist_ok(a)) a.fold = 0;
     return a;
 }
 
@@ -1904,7 +1898,7 @@ extern "C" int l3_set_decode_horizon(l3_ctx* c, int32_t end_pos) {
 
 extern "C" int l3_decode_persistent(l3_ctx* c, int32_t* active) {
     CHECK_CTX(c);
-    if (active) *active = c->dec_exec && c->persist_graph ? (c->persist.fold ? 2 : 1) : 0;
+    if (active) *active = c->dec_exec && c->persist_graph ? 1 : 0;
     return 0;
 }
 

@@ -389,13 +389,6 @@ class Context:
         check(lib().l3_decode_persistent(self._h, ctypes.byref(v)))
         return bool(v.value)
 
-    def decode_fold(self) -> bool:
-        """True when the persistent step runs the fold layout (L3_DECODE_PERSIST_FOLD: head
-        workgroups compute their own q / k / v rows, no QKV hand-off)."""
-        v = ctypes.c_int32(0)
-        check(lib().l3_decode_persistent(self._h, ctypes.byref(v)))
-        return v.value == 2
-
     def decode_recoveries(self) -> int:
         """Persistent decode steps that gave up on a hand-off and were re-run on the graph path."""
         v = ctypes.c_int64(0)

@@ -46,24 +46,21 @@ def _dream(g):
             int(g["dream_max_new"]))
 
 
-@pytest.mark.parametrize("persist", ["1", "0", "fold"])
+@pytest.mark.parametrize("persist", ["1", "0"])
 @pytest.mark.parametrize("preset", ["default", "sharp"])
 def test_decode_values_match_reference(tmpdir_mod, monkeypatch, preset, persist):
     """Each greedy step's winning logit (the value np.argmax picked, llama3.py:320) against the
     reference's, over all 145 steps: the persistent step (one launch per step, values from its
-    lm_head partials; "fold": its fold layout) and the 25-kernel graph (values from its argmax
-    kernels), in the device loop.  Default preset: within 1e-4; sharp (|logits| ~ 33): 1e-4 +
-    2e-4 |ref|.  Reports the smallest top-2 margin of the run (the reference's), i.e. how close
-    an id came to flipping."""
-    monkeypatch.setenv("L3_DECODE_PERSIST", "0" if persist == "0" else "1")
-    monkeypatch.setenv("L3_DECODE_PERSIST_FOLD", "1" if persist == "fold" else "0")
+    lm_head partials) and the 25-kernel graph (values from its argmax kernels), in the device
+    loop.  Default preset: within 1e-4; sharp (|logits| ~ 33): 1e-4 + 2e-4 |ref|.  Reports the
+    smallest top-2 margin of the run (the reference's), i.e. how close an id came to flipping."""
+    monkeypatch.setenv("L3_DECODE_PERSIST", persist)
     g, args, path = _stories(tmpdir_mod, preset)
     prompt, want, n = _dream(g)
     m = llama3.Llama(path, args)
     ids, vals = m.context.greedy_generate(prompt, n, values=True)
     np.testing.assert_array_equal(ids, want)
-    assert m.context.decode_persistent() == (persist != "0")
-    assert m.context.decode_fold() == (persist == "fold")
+    assert m.context.decode_persistent() == (persist == "1")
     ref = np.asarray(g["dream_max"]).reshape(1, -1)
     err = np.abs(vals.astype(np.float64) - ref)
     tol = ATOL + (RTOL * np.abs(ref) if preset == "sharp" else 0.0)
@@ -169,59 +166,6 @@ def test_persistent_decode_fault_in_abandoned_run_ahead(tmpdir_mod, monkeypatch)
     del gen
     np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
     assert m.context.decode_recoveries() == 1
-
-
-@pytest.mark.parametrize("fold", ["1", "2"])
-@pytest.mark.parametrize("preset", ["default", "sharp"])
-def test_persistent_decode_fold_bit_identical(tmpdir_mod, monkeypatch, preset, fold):
-    """The fold layout (L3_DECODE_PERSIST_FOLD=1: each head workgroup computes its own q / k / v
-    rows from Wqkv rows it holds in LDS, no QKV hand-off) does the arithmetic of the QKV stage it
-    replaces in the same order; the compiler packs some of its f32 multiplies differently
-    (v_pk_mul + add against a fused multiply-add), so the values agree to a few ulp, not bit for
-    bit (measured: 92 of 145 steps identical, max 3.6e-7 on |logit| ~ 1.4): every id equals
-    the plain persistent step's and the reference's, in the device loop and the lazy generator,
-    and every value is within 1e-6 (+ 1e-6 relative) of the plain step's."""
-    g, args, path = _stories(tmpdir_mod, preset)
-    prompt, want, n = _dream(g)
-    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
-    monkeypatch.setenv("L3_DECODE_PERSIST_FOLD", "0")
-    ids0, vals0 = llama3.Llama(path, args).context.greedy_generate(prompt, n, values=True)
-    monkeypatch.setenv("L3_DECODE_PERSIST_FOLD", fold)
-    m = llama3.Llama(path, args)
-    ids1, vals1 = m.context.greedy_generate(prompt, n, values=True)
-    assert m.context.decode_fold()
-    np.testing.assert_array_equal(ids1, want)
-    np.testing.assert_array_equal(ids1, ids0)
-    err = np.abs(vals1.astype(np.float64) - vals0)
-    assert (err <= 1e-6 + 1e-6 * np.abs(vals0)).all(), f"max {err.max():.2e}"
-    print(f"{preset} fold {fold}: vs the plain persistent step: {int((err == 0).sum())} / {err.size} values identical, max {err.max():.2e}")
-    np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
-    assert m.context.decode_recoveries() == 0
-
-
-@pytest.mark.parametrize("fold", ["1", "2"])
-@pytest.mark.parametrize("fault_pos,fault_wg", FAULTS)
-def test_persistent_decode_fold_fault_recovers(tmpdir_mod, monkeypatch, fault_pos, fault_wg, fold):
-    """A give-up in the fold layout — by head workgroup 1 (its K / V rows are written only after
-    its last wait: none of the step's slots) or by an lm workgroup (the layers complete, every
-    slot written) — recovers on the graph path with the reference's ids and values, in the
-    device loop and the lazy generator."""
-    g, args, path = _stories(tmpdir_mod, "sharp")
-    prompt, want, n = _dream(g)
-    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
-    monkeypatch.setenv("L3_DECODE_PERSIST_FOLD", fold)
-    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", str(fault_pos))
-    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
-    m = llama3.Llama(path, args)
-    ids, vals = m.context.greedy_generate(prompt, n, values=True)
-    np.testing.assert_array_equal(ids, want)
-    ref = np.asarray(g["dream_max"]).reshape(1, -1)
-    assert (np.abs(vals - ref) <= ATOL + RTOL * np.abs(ref)).all()
-    assert m.context.decode_recoveries() == 1
-    assert not m.context.decode_persistent()
-    m2 = llama3.Llama(path, args)
-    np.testing.assert_array_equal(np.concatenate(list(m2.generate(prompt, n)), axis=1), want)
-    assert m2.context.decode_recoveries() == 1
 
 
 def test_persistent_decode_hd64_instance(tmpdir_mod, monkeypatch):
