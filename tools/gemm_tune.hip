@@ -62,6 +62,27 @@ static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
     for (auto& x : v) x = lo + (hi - lo) * (float)rand() / (float)RAND_MAX;
 }
 
+// cold mode (g_cold): every launch follows a kernel that reads 96 MB, so the weights and inputs
+// come from the MALL / HBM as in the batched decode loop (each XCD's 4 MB L2 evicted); per-launch
+// time = (flush + launch) - flush alone, both timed over the same iterations
+static bool g_cold = false;
+__global__ void flush_kernel(const f32x4* buf, int64_t n, float* sink) {
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) a += buf[i];
+    if (a.x + a.y + a.z + a.w == 12345.f) sink[0] = a.x;
+}
+static f32x4* g_flush = nullptr;
+static float* g_sink = nullptr;
+static const int64_t FLUSH_N = (96ll << 20) / 16;
+static void flush(hipStream_t s) {
+    if (!g_flush) {
+        CK(hipMalloc(&g_flush, FLUSH_N * 16));
+        CK(hipMemset(g_flush, 0, FLUSH_N * 16));
+        CK(hipMalloc(&g_sink, 4));
+    }
+    hipLaunchKernelGGL(flush_kernel, dim3(2048), dim3(256), 0, s, g_flush, FLUSH_N, g_sink);
+}
+
 static void run_shape(const char* label, int epi, int M, int K, int N, bool norm,
                       std::vector<Variant> vars, int rounds, int iters) {
     const int outN = epi == EPI_SWIGLU ? N / 2 : (epi == EPI_QKV ? 288 : N);
@@ -130,13 +151,25 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int r = 0; r < rounds + 1; ++r) {
+        float fl_ms = 0;
+        if (g_cold) {  // the flushes alone
+            CK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i) flush(s);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&fl_ms, e0, e1));
+        }
         for (size_t v = 0; v < vars.size(); ++v) {
             CK(hipEventRecord(e0, s));
-            for (int i = 0; i < iters; ++i) vars[v].run(g, s);
+            for (int i = 0; i < iters; ++i) {
+                if (g_cold) flush(s);
+                vars[v].run(g, s);
+            }
             CK(hipEventRecord(e1, s));
             CK(hipEventSynchronize(e1));
             float ms = 0;
             CK(hipEventElapsedTime(&ms, e0, e1));
+            ms -= fl_ms;
             if (r) tf[v].push_back(flops * iters / (ms * 1e-3) / 1e12);  // round 0 = warm-up
         }
     }
@@ -264,6 +297,21 @@ int main(int argc, char** argv) {
         run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
                   {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 3, 4, 4, EPI_SWIGLU, 3, 16),
                    GVAR(2, 3, 4, 4, EPI_SWIGLU, 2, 16)}, rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "skinnycold") {  // batched decode GEMMs, each launch after an L2 flush
+        g_cold = true;
+        for (int Ms : {64, 256}) {
+            char l[64];
+            snprintf(l, sizeof l, "M=%d QKV", Ms);
+            run_shape(l, EPI_QKV, Ms, 288, 864, true, {SVAR(EPI_QKV, 1, 2), SVAR(EPI_QKV, 1, 6)}, rounds, iters);
+            snprintf(l, sizeof l, "M=%d gate|up", Ms);
+            run_shape(l, EPI_SWIGLU, Ms, 288, 1536, true, {SVAR(EPI_SWIGLU, 2, 2)}, rounds, iters);
+            snprintf(l, sizeof l, "M=%d O-proj", Ms);
+            run_shape(l, EPI_RESID, Ms, 288, 288, false, {SVAR(EPI_RESID, 1, 2)}, rounds, iters);
+            snprintf(l, sizeof l, "M=%d down", Ms);
+            run_shape(l, EPI_RESID, Ms, 768, 288, false, {SVAR(EPI_RESID, 1, 2)}, rounds, iters);
+        }
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "skinny") {  // batched decode: the layer GEMMs at M = B
