@@ -342,6 +342,23 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "wide") {  // 64 x 96 wave tiles: 24 MFMAs per 4-deep k-step
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(2, 1, 4, 6, EPI_QKV, 4, 16),
+                   GVAR(2, 1, 4, 6, EPI_QKV, 3, 16), GVAR(4, 1, 4, 6, EPI_QKV, 2, 16),
+                   GVAR(2, 1, 4, 6, EPI_QKV, 4, 32), GVAR(1, 1, 4, 6, EPI_QKV, 4, 16)}, rounds, iters);
+        run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
+                  {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), GVAR(2, 1, 2, 6, EPI_RESID, 4, 32),
+                   GVAR(2, 1, 4, 6, EPI_RESID, 4, 32), GVAR(2, 1, 4, 6, EPI_RESID, 3, 16),
+                   GVAR(1, 1, 4, 6, EPI_RESID, 4, 32)}, rounds, iters);
+        run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
+                  {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(2, 1, 4, 6, EPI_RESID, 3, 32),
+                   GVAR(2, 1, 4, 6, EPI_RESID, 2, 32), GVAR(4, 1, 4, 6, EPI_RESID, 2, 16)}, rounds, iters);
+        run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 1, 4, 8, EPI_SWIGLU, 3, 16),
+                   GVAR(2, 1, 4, 8, EPI_SWIGLU, 2, 16)}, rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "qkv18") {  // QKV wave tiles with more MFMAs per k-step
         // 64 x 48 wave tiles issue 12 MFMAs per 4-deep k-step; 96 x 48 (192 x 96 blocks) 18 and
         // 128 x 32 (3-wave 128 x 96 blocks) 16, both dividing N = 864 without padding
