@@ -192,6 +192,37 @@ def test_persistent_decode_hd64_instance(tmpdir_mod, monkeypatch):
     assert not m0.context.decode_persistent()
 
 
+def test_persistent_decode_past_256_keys(tmpdir_mod, monkeypatch):
+    """Contexts longer than the persistent step's 256-thread workgroup (max_seq_len 700): the
+    attention stage's second-pass loops (scores of keys past the first 256 and their P.V rows
+    read from the cache) run for every step past position 256.  A 693-step greedy run from a
+    7-token prompt — ids and each step's winning logit against the oracle (smallest top-2
+    margin of this run 6.9e-3, |logits| <= 12.7) — on the persistent step in the device loop
+    and the lazy generator, and on the 25-kernel graph."""
+    args = ModelArgs(dim=64, n_layers=2, n_heads=2, n_kv_heads=1, vocab_size=512, max_seq_len=700,
+                     max_batch_size=1)
+    w = synth.make_weights(args, 128, seed=22, preset="sharp")
+    path = os.path.join(tmpdir_mod, "long.npz")
+    synth.save_npz(path, w)
+    prompt = np.random.default_rng(5).integers(0, args.vocab_size, (1, 7))
+    n = args.max_seq_len
+    want, wv = _oracle_greedy_values(orc.OracleModel(w, args), prompt, n)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    m = llama3.Llama(path, args)
+    ids, vals = m.context.greedy_generate(prompt, n, values=True)
+    assert m.context.decode_persistent()
+    np.testing.assert_array_equal(ids, want)
+    err = np.abs(vals.astype(np.float64) - wv)
+    assert (err <= ATOL + RTOL * np.abs(wv)).all(), f"worst step {int(err.argmax())}: {err.max():.3e}"
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
+    assert m.context.decode_recoveries() == 0
+    monkeypatch.setenv("L3_DECODE_PERSIST", "0")
+    m0 = llama3.Llama(path, args)
+    np.testing.assert_array_equal(m0.generate_all(prompt, n), want)
+    assert not m0.context.decode_persistent()
+    print(f"693 steps past 256 keys: ids exact, values max-abs {err.max():.2e}")
+
+
 def _oracle_greedy_values(ref, prompt, max_new):
     """The reference's greedy loop (llama3.py:310-321) on the oracle, with each step's winning
     logit (the value np.argmax picked at :320)."""
