@@ -192,6 +192,34 @@ def test_persistent_decode_hd64_instance(tmpdir_mod, monkeypatch):
     assert not m0.context.decode_persistent()
 
 
+# (dim, heads, kv heads, hidden, seed) -> the persistent step's instances by their (D, FD)
+# chunking (decode_persist.hip L3_PERSIST_INSTANCES): (1, 12), (5, 3), (5, 16), (8, 16), (8, 12);
+# the seeds' smallest top-2 margins over the run are 0.023 / 0.023 / 0.055 / 0.035 / 0.071
+INSTANCE_SHAPES = [(64, 1, 1, 512, 32), (128, 2, 2, 128, 33), (256, 4, 4, 1024, 32), (512, 8, 4, 1024, 32),
+                   (384, 8, 8, 768, 31)]
+
+
+@pytest.mark.parametrize("dim,heads,kv_heads,hidden,seed", INSTANCE_SHAPES)
+def test_persistent_decode_instances(tmpdir_mod, monkeypatch, dim, heads, kv_heads, hidden, seed):
+    """Every persistent-step instance the stories15M / tiny tests do not reach: 91 greedy steps
+    (max_seq_len 96) on the persistent step, ids and winning logits against the oracle."""
+    args = ModelArgs(dim=dim, n_layers=2, n_heads=heads, n_kv_heads=kv_heads, vocab_size=512, max_seq_len=96,
+                     max_batch_size=1)
+    w = synth.make_weights(args, hidden, seed=seed, preset="sharp")
+    path = os.path.join(tmpdir_mod, f"inst{dim}_{hidden}.npz")
+    synth.save_npz(path, w)
+    prompt = np.random.default_rng(seed).integers(0, args.vocab_size, (1, 5))
+    n = args.max_seq_len
+    want, wv = _oracle_greedy_values(orc.OracleModel(w, args), prompt, n)
+    monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    m = llama3.Llama(path, args)
+    ids, vals = m.context.greedy_generate(prompt, n, values=True)
+    assert m.context.decode_persistent()
+    np.testing.assert_array_equal(ids, want)
+    err = np.abs(vals.astype(np.float64) - wv)
+    assert (err <= ATOL + RTOL * np.abs(wv)).all(), f"worst step {int(err.argmax())}: {err.max():.3e}"
+
+
 def test_persistent_decode_past_256_keys(tmpdir_mod, monkeypatch):
     """Contexts longer than the persistent step's 256-thread workgroup (max_seq_len 700): the
     attention stage's second-pass loops (scores of keys past the first 256 and their P.V rows
