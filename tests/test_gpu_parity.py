@@ -1193,3 +1193,28 @@ def test_persistent_decode_step_matches_golden(tmpdir_mod, monkeypatch, preset):
         del gen
         np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
         assert m.context.decode_stats()["graph_steps"] > 0
+
+
+@pytest.mark.parametrize("persist", ["1", "0"])
+def test_generate_schedule_edges(tmpdir_mod, monkeypatch, persist):
+    """The reference loop's edges (llama3.py:310-321), as call sequences on one model whose cache
+    persists across calls (:138-153): max_new_tokens <= L runs nothing — no prefill, so the
+    cache is untouched — max_new_tokens == L + 1 is the prefill's id alone, L + 2 the first
+    decode step across the hole, a 1-token prompt; then a shorter prompt whose decode hole sees
+    the earlier calls' stale slots.  Every call's ids (lazy and device loop, B = 1 and B = 3)
+    against the oracle driven through the same sequence."""
+    from config import ModelArgs
+    monkeypatch.setenv("L3_DECODE_PERSIST", persist)
+    args = ModelArgs(dim=64, n_layers=2, n_heads=4, n_kv_heads=2, vocab_size=512, max_seq_len=64, max_batch_size=3)
+    w, path = _model(tmpdir_mod, args, 192, 77, "sharp")
+    rng = np.random.default_rng(8)
+    for B in (1, 3):
+        m, ref = llama3.Llama(path, args), orc.OracleModel(w, args)
+        p10, p5, p1 = (rng.integers(0, args.vocab_size, (B, n)) for n in (10, 5, 1))
+        calls = [(p10, 30), (p10, 10), (p10, 4), (p10, 11), (p10, 12), (p1, 9), (p5, 20), (p5, 5)]
+        for k, (p, n) in enumerate(calls):
+            want = list(ref.generate(p, n))
+            want = np.concatenate(want, axis=1) if want else np.empty((B, 0), np.int64)
+            got = m.generate_all(p, n) if k % 2 else np.concatenate(list(m.generate(p, n)) or [np.empty((B, 0), np.int64)], axis=1)
+            assert got.shape == want.shape, (k, got.shape, want.shape)
+            np.testing.assert_array_equal(got, want, err_msg=f"B={B} call {k}: L={p.shape[1]} max_new={n}")
