@@ -25,7 +25,9 @@ if "--read" not in sys.argv:
         p = os.path.join(d, "w.npz")
         synth.save_npz(p, w)
         m = llama3.Llama(p, args)
-    m.generate_all(np.array([[1, 76, 505, 263, 12561]]), 150)
+    # --max-new N: e.g. 143 = 5 + 2 eager steps + 17 graphs of 8 (the last launch a multi-step one)
+    max_new = int(sys.argv[sys.argv.index("--max-new") + 1]) if "--max-new" in sys.argv else 150
+    m.generate_all(np.array([[1, 76, 505, 263, 12561]]), max_new)
 st = np.fromfile(path, dtype=np.uint64).reshape(256, 128).astype(np.int64)
 xcc = st[:, 127].copy()
 st[:, 127] = 0
