@@ -69,7 +69,7 @@ for s in "$@"; do
     decode16) L3_GEMV_LPU=16 step decode16 300 python tools/bench_decode.py ;;
     decprofb*) step $s 300 rocprofv3 --kernel-trace --stats -d gpurun_out/$s -o run --output-format csv -- python tools/bench_decode.py --eager-batch ${s#decprofb} ;;
     decprofp) step decprofp 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprofp -o run --output-format csv -- python tools/bench_decode.py ;;
-    persistab) step persistab 600 bash tools/ab_lib.sh "tree:1 tree:0 tree:2" 3 ;;
+    persistab) step persistab 600 bash tools/ab_lib.sh "tree:1 tree:0" 3 ;;
     decprof) step decprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/decprof -o run --output-format csv -- python tools/bench_decode.py --eager ;;
     c5) step c5 900 python bench.py --workload c5 --steps 1 --warmup 1 ;;
     c4) step c4 300 python bench.py --global-batch 2048 --steps 5 --warmup 1 --no-cpu-baseline --no-kernel-breakdown ;;
