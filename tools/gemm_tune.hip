@@ -304,13 +304,17 @@ int main(int argc, char** argv) {
         for (int Ms : {64, 256}) {
             char l[64];
             snprintf(l, sizeof l, "M=%d QKV", Ms);
-            run_shape(l, EPI_QKV, Ms, 288, 864, true, {SVAR(EPI_QKV, 1, 2), SVAR(EPI_QKV, 1, 6)}, rounds, iters);
+            run_shape(l, EPI_QKV, Ms, 288, 864, true,
+                      {SVAR(EPI_QKV, 1, 2), SVAR(EPI_QKV, 1, 3), SVAR(EPI_QKV, 1, 4), SVAR(EPI_QKV, 1, 6)}, rounds, iters);
             snprintf(l, sizeof l, "M=%d gate|up", Ms);
-            run_shape(l, EPI_SWIGLU, Ms, 288, 1536, true, {SVAR(EPI_SWIGLU, 2, 2)}, rounds, iters);
+            run_shape(l, EPI_SWIGLU, Ms, 288, 1536, true,
+                      {SVAR(EPI_SWIGLU, 2, 2), SVAR(EPI_SWIGLU, 2, 3), SVAR(EPI_SWIGLU, 2, 4)}, rounds, iters);
             snprintf(l, sizeof l, "M=%d O-proj", Ms);
-            run_shape(l, EPI_RESID, Ms, 288, 288, false, {SVAR(EPI_RESID, 1, 2)}, rounds, iters);
+            run_shape(l, EPI_RESID, Ms, 288, 288, false,
+                      {SVAR(EPI_RESID, 1, 2), SVAR(EPI_RESID, 1, 3), SVAR(EPI_RESID, 1, 4)}, rounds, iters);
             snprintf(l, sizeof l, "M=%d down", Ms);
-            run_shape(l, EPI_RESID, Ms, 768, 288, false, {SVAR(EPI_RESID, 1, 2)}, rounds, iters);
+            run_shape(l, EPI_RESID, Ms, 768, 288, false,
+                      {SVAR(EPI_RESID, 1, 2), SVAR(EPI_RESID, 1, 3), SVAR(EPI_RESID, 1, 4), SVAR(EPI_RESID, 1, 6)}, rounds, iters);
         }
         return 0;
     }
