@@ -615,6 +615,26 @@ def test_generate_all_batched_matches_oracle(tmpdir_mod):
             np.testing.assert_array_equal(got, orc.greedy_ids(ref, prompt, n))
 
 
+def test_decode_shrinking_batches_against_oracle(tmpdir_mod):
+    """L = 1 steps whose batch shrinks from call to call (64 -> 33 -> 5 -> 2 rows: the skinny
+    MFMA and GEMV O-proj / FFN paths, rows < B never skipping a position) against the oracle's
+    logits (llama3.py:163-211), then the batched device loop on the same context."""
+    args = synth.stories15m(64)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 7, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(8)
+    ids = rng.integers(0, args.vocab_size, (64, 9))
+    _close(m(ids, 0), ref(ids, 0))
+    pos = 9
+    for B in (64, 33, 33, 5, 3, 2, 2):  # shrinking: rows < B never skip a position
+        nxt = rng.integers(0, args.vocab_size, (B, 1))
+        _close(m(nxt, pos), ref(nxt, pos))
+        pos += 1
+    prompt = rng.integers(0, args.vocab_size, (6, 4))
+    np.testing.assert_array_equal(m.generate_all(prompt, 30), orc.greedy_ids(ref, prompt, 30))
+
+
 @pytest.mark.parametrize("dim,heads,kv_heads", [(512, 4, 1), (128, 4, 2), (192, 2, 1)])
 def test_head_dims_gqa_decode_with_norm_weights(tmpdir_mod, dim, heads, kv_heads):
     """Head geometries beyond stories15M's 48 — HD = 128 (Llama-3, n_rep = 4), 32 and 96 — with
