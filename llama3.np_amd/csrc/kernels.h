@@ -11,13 +11,14 @@ namespace l3 {
 //   runtime.hip  L3_BATCH_SPLIT (2), L3_LAST_LAYER_ALL_ROWS (0), L3_DECODE_FUSE_O (1),
 //                L3_LM_AMAX (1), L3_DECODE_FOLD_ARGMAX (1), L3_DECODE_SPECULATE (1), L3_DECODE_GRAPH_STEPS (8),
 //                L3_DECODE_GRAPH (1), L3_COMM_MODE (1), L3_COMM_PRIORITY (1), L3_GROUP_MULTI_PATH (0),
-//                L3_DECODE_PERSIST (1 persistent step; 0 graph)
+//                L3_DECODE_PERSIST (1 persistent step; 0 graph), L3_DECODE_ROWS_AMAX (1)
 //   test knobs   L3_DECODE_PERSIST_MAX_CUS (cap the CUs the persistent step sees), L3_DECODE_PERSIST_FAULT
 //                (a workgroup gives up in the step at that position; L3_DECODE_PERSIST_FAULT_WG which),
-//                L3_GROUP_VIRTUAL (a group's members may share one device; D2D copies for the gather)
+//                L3_GROUP_VIRTUAL (a group's members may share one device; D2D copies for the gather),
+//                L3_DECODE_PERSIST_STAMPS=<file> (diagnostic timeline, tools/persist_stamps.py)
 //   gemm.hip     L3_SPLITK (1), L3_SPLITK_CFG (0), L3_SPLITK_BLOCKS (1024), L3_SPLITK_MINKT (8),
 //                L3_GEMV_NT (1), L3_GEMV_LPU (0 = by shape), L3_GEMV_MR (by shape), L3_SKINNY (1),
-//                L3_SKINNY_MIN (9)
+//                L3_SKINNY_MIN (9), L3_SKINNY_CH (2), L3_SKINNY_TN2_MIN (256)
 inline int env_knob(const char* name, int def) {
     const char* e = getenv(name);
     return e && *e ? atoi(e) : def;
