@@ -414,12 +414,16 @@ int main(int argc, char** argv) {
     } else {
     // Llama-3-8B shapes (C5) at M = 16384 rows (tuning size)
     const int Mc = 16384;
+    // round 5: + 8-wave 256 x 128 / 128 x 256 blocks (half the LDS fragment traffic per MFMA of
+    // the 128 x 128 block) and deeper k-tile rings, for the long-K (4096) shapes
     run_shape("C5 gate|up", EPI_SWIGLU, Mc, 4096, 28672, true,
-              {RVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16),
-               GVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, 3);
+              {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(2, 2, 4, 4, EPI_SWIGLU, 2, 32),
+               GVARN(2, 2, 4, 4, EPI_SWIGLU, 3, 16, 3), GVAR(4, 2, 4, 4, EPI_SWIGLU, 2, 16),
+               GVAR(4, 2, 4, 4, EPI_SWIGLU, 1, 32), GVAR(2, 4, 4, 4, EPI_SWIGLU, 2, 16)}, rounds, 3);
     run_shape("C5 QKV-shape (store)", EPI_STORE, Mc, 4096, 6144, true,
               {GVAR(2, 2, 4, 4, EPI_STORE, 3, 16), GVAR(2, 2, 4, 3, EPI_STORE, 4, 16),
-               GVAR(2, 2, 4, 4, EPI_STORE, 2, 32)}, rounds, 3);
+               GVAR(2, 2, 4, 4, EPI_STORE, 2, 32), GVAR(4, 2, 4, 4, EPI_STORE, 2, 16),
+               GVAR(2, 4, 4, 4, EPI_STORE, 2, 16)}, rounds, 3);
     run_shape("C5 O-proj", EPI_RESID, Mc, 4096, 4096, false,
               {GVAR(2, 2, 4, 4, EPI_RESID, 3, 16), GVAR(2, 2, 4, 4, EPI_RESID, 2, 32)}, rounds, 3);
     run_shape("C5 down", EPI_RESID, Mc, 14336, 4096, false,
