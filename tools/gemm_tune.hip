@@ -346,6 +346,24 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "big8") {  // round 5: 8-wave blocks at the C3 shapes
+        // the product's 64 x 64 / 64 x 48 wave tiles in 256 x 128 (4 x 2 waves) and 128 x 256
+        // (2 x 4) blocks: a staged A / W piece feeds twice the MFMAs of the 4-wave block's
+        run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVAR(4, 2, 4, 4, EPI_SWIGLU, 2, 16),
+                   GVAR(4, 2, 4, 4, EPI_SWIGLU, 1, 16), GVAR(2, 4, 4, 4, EPI_SWIGLU, 2, 16),
+                   GVAR(4, 2, 4, 4, EPI_SWIGLU, 2, 32)}, rounds, iters);
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(4, 2, 4, 3, EPI_QKV, 2, 16),
+                   GVAR(2, 4, 4, 3, EPI_QKV, 2, 16)}, rounds, iters);
+        run_shape("down (+resid)", EPI_RESID, M, 768, 288, false,
+                  {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), GVAR(4, 2, 4, 3, EPI_RESID, 2, 32),
+                   GVAR(4, 2, 4, 3, EPI_RESID, 2, 16)}, rounds, iters);
+        run_shape("O-proj (+resid)", EPI_RESID, M, 288, 288, false,
+                  {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), GVAR(4, 2, 2, 3, EPI_RESID, 2, 32),
+                   GVAR(4, 2, 2, 3, EPI_RESID, 3, 32)}, rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "wide") {  // 64 x 96 wave tiles: 24 MFMAs per 4-deep k-step
         run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
                   {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(2, 1, 4, 6, EPI_QKV, 4, 16),
