@@ -215,6 +215,16 @@ int l3_decode_stats(l3_ctx* ctx, int64_t* graph_steps, int64_t* speculative_hits
 int l3_decode_persistent(l3_ctx* ctx, int32_t* active);
 /* Persistent decode steps recovered on the graph path over the context's life (see above). */
 int l3_decode_recoveries(l3_ctx* ctx, int64_t* count);
+/* Device bounds checks (no reference counterpart; SURVEY.md §5 "device bounds asserts in a debug
+ * build"): in the check build (libllama3hip_check.so, `make -C llama3.np_amd/csrc check-lib`;
+ * load it with L3_LIB_PATH) every kernel counts the indices that leave their buffers —
+ * counts[0] K / V cache slots outside [0, max_seq_len), counts[1] attention launches whose keys
+ * pass max_seq_len, counts[2] token ids outside the vocabulary, counts[3] reserved — and this
+ * returns the counts of the context's device since the last call (then clears them);
+ * *enabled = 1 in the check build, 0 in the release library (whose counts stay 0).
+ * l3_device_check_selftest records one of each of the first three classes (plumbing check). */
+int l3_device_check_counts(l3_ctx* ctx, uint32_t* counts, int32_t* enabled);
+int l3_device_check_selftest(l3_ctx* ctx);
 /* Lazy greedy decode runs up to 16 steps ahead of the caller on the device (undone if the
  * caller leaves the schedule, so results are unchanged), and at most ~4 ms of decode work by
  * the measured step time: a caller that stops early (EOS, an abandoned generator) or makes any

@@ -75,6 +75,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     const int q_hi = min(p.L, q_lo + QW);
     const int key_end = start_pos + q_hi;  // keys [0, key_end) are needed
     const int ntiles = (key_end + KT - 1) / KT;
+    if (threadIdx.x == 0) L3_DCHECK(start_pos >= 0 && start_pos + p.L <= p.Smax, CHK_ATTN_KEYS);
 
     // Loads are unpredicated, from clamped (in-bounds) rows: a query lane past L computes on a
     // copy of row L - 1 and is never stored (each lane's softmax state is its own query's), and
@@ -271,6 +272,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs p) {
     const int kvh = h / (p.H / p.KVH);
     const int pos = start_of(p);
     const int S = pos + 1;
+    if (tid == 0) L3_DCHECK(pos >= 0 && S <= p.Smax, CHK_ATTN_KEYS);
     const int64_t kv_base = ((int64_t)b * p.KVH + kvh) * p.Smax * HD;
     const f32x4* K4 = reinterpret_cast<const f32x4*>(p.cache_k + kv_base);
     const f32x4* V4 = reinterpret_cast<const f32x4*>(p.cache_v + kv_base);

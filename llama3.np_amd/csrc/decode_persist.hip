@@ -346,6 +346,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
         }
         id = bi;
         if (wg == 0 && tid == 0) {  // the previous step's id (and its logit): its generate history entry
+            L3_DCHECK(id >= 0 && id < p.VS, CHK_TOKEN_ID);
             const int q = pos - 1 - hist_base;
             if (hist && q >= 0 && q < hist_cap) hist[q] = id;
             if (hist_val && q >= 0 && q < hist_cap) hist_val[q] = best;
@@ -685,6 +686,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int cc = col - (sec == 1 ? qdim : qdim + kvdim);
             const int head = cc / HD, d = cc - head * HD;
             const int64_t coff = ((int64_t)head * p.Smax + pos) * HD + d;
+            L3_DCHECK(pos >= 0 && pos < p.Smax, CHK_KV_SLOT);
             const int64_t boff = (((int64_t)(pos % KV_BAK_SLOTS) * 2 + sec - 1) * KVH + head) * HD + d;
             float* const* cache = sec == 1 ? p.cache_k : p.cache_v;
             for (int li = 0; li < p.n_layers; ++li) {
@@ -831,5 +833,7 @@ hipError_t launch_decode_persist(const DecodePersistArgs& a, int grid, hipStream
 #undef L3_LAUNCH
     return hipErrorNotSupported;
 }
+
+hipError_t dcheck_collect_persist(unsigned* out) { return dcheck_collect(out); }
 
 }  // namespace l3

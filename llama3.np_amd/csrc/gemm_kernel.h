@@ -154,6 +154,7 @@ __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&ac
                 const int64_t off = sec[j] == 0
                                         ? (int64_t)row * qdim + col
                                         : (((int64_t)bidx[i] * p.KVH + head[j]) * p.Smax + pos[i]) * p.HD + d[j];
+                L3_DCHECK(sec[j] == 0 || (pos[i] >= 0 && pos[i] < p.Smax), CHK_KV_SLOT);
                 *reinterpret_cast<f32x4*>(base + off) = r;
             }
         }
@@ -326,6 +327,7 @@ __global__ void __launch_bounds__(256) splitk_finish_kernel(GemmArgs p) {
         float* base = sec == 0 ? p.q_out : (sec == 1 ? p.cache_k : p.cache_v);
         const int64_t off = sec == 0 ? (int64_t)row * qdim + col
                                      : (((int64_t)bidx * p.KVH + head) * p.Smax + pos) * p.HD + d;
+        L3_DCHECK(sec == 0 || (pos >= 0 && pos < p.Smax), CHK_KV_SLOT);
         *reinterpret_cast<f32x4*>(base + off) = r;
     } else {
         const int col = 4 * c4;
@@ -1049,6 +1051,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemmArgs p) {
             if (p.kv_bak && qkv_sec > 0)  // [pos % KV_BAK_SLOTS][k, v][batch row][KV head][HD]
                 *reinterpret_cast<float2*>(p.kv_bak + (((((int64_t)(pos % KV_BAK_SLOTS) * 2 + qkv_sec - 1) * (p.M / p.L) + bidx) *
                                                         p.KVH + qkv_head) * p.HD + qkv_d)) = bak_old[mi];
+            L3_DCHECK(qkv_sec == 0 || (pos >= 0 && pos < p.Smax), CHK_KV_SLOT);
             *dst = qkv_sec == 0 ? float2{r0 * p.q_scale, r1 * p.q_scale} : float2{r0, r1};
         } else {
             float* dst = p.C + (int64_t)m * p.ldc + unit;

@@ -24,6 +24,36 @@ inline int env_knob(const char* name, int def) {
     return e && *e ? atoi(e) : def;
 }
 
+// Device bounds checks (SURVEY §5 "device bounds asserts in a debug build"): built with
+// -DL3_DEVICE_CHECKS (libllama3hip_check.so, `make check-lib`), the kernels count, per class,
+// every index that leaves the buffer it addresses — in counters, not traps, so a violation is
+// reported by l3_device_check_counts instead of faulting the device.  The release library
+// compiles them away.  Classes: a K / V cache slot (position outside [0, Smax)), an attention
+// launch's key range (start_pos + L > Smax), a token id out of [0, n) (argmax results, the
+// embedding rows the lm_head partials select).
+enum CheckClass : int { CHK_KV_SLOT = 0, CHK_ATTN_KEYS = 1, CHK_TOKEN_ID = 2, CHK_N = 4 };
+#ifdef L3_DEVICE_CHECKS
+static __device__ unsigned l3_dcheck_counts[CHK_N];  // one set per translation unit
+#define L3_DCHECK(cond, cls)                                                      \
+    do {                                                                          \
+        if (!(cond)) atomicAdd(&::l3::l3_dcheck_counts[(cls)], 1u);               \
+    } while (0)
+// this translation unit's counters, added into out[CHK_N], then cleared
+static inline hipError_t dcheck_collect(unsigned* out) {
+    unsigned h[CHK_N] = {};
+    hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(l3_dcheck_counts), sizeof h, 0, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    for (int i = 0; i < CHK_N; ++i) out[i] += h[i];
+    const unsigned z[CHK_N] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(l3_dcheck_counts), z, sizeof z, 0, hipMemcpyHostToDevice);
+}
+#define L3_DCHECK_ON 1
+#else
+#define L3_DCHECK(cond, cls) ((void)0)
+static inline hipError_t dcheck_collect(unsigned*) { return hipSuccess; }
+#define L3_DCHECK_ON 0
+#endif
+
 // Epilogues of the NT GEMM  C[M,N] = A[M,K] * W[N,K]^T  (see gemm.hip).
 enum Epilogue : int {
     EPI_STORE = 0,   // C = s_row * acc
@@ -328,6 +358,12 @@ hipError_t launch_fold_cols(float* W, int64_t rows, int K, const float* w, hipSt
 // cache[b][h][pos][:] = bak[b][h][:] for b < B, h < KVH (undo of a speculative decode step)
 hipError_t launch_kv_restore(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos,
                              hipStream_t s);
+// device bounds-check counters of each translation unit (L3_DEVICE_CHECKS builds; else no-ops)
+hipError_t dcheck_collect_gemm(unsigned* out);
+hipError_t dcheck_collect_attention(unsigned* out);
+hipError_t dcheck_collect_misc(unsigned* out);
+hipError_t dcheck_collect_persist(unsigned* out);
+hipError_t launch_dcheck_selftest(hipStream_t s);
 hipError_t launch_rope(const float* x, float* y, const float* cos_t, const float* sin_t, int B,
                        int L, int nh, int hd, hipStream_t s);
 

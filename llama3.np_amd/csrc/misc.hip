@@ -29,7 +29,7 @@ __device__ __forceinline__ float wave_max(float v) {
 // hist_off 1: the step's lm_head has already moved the position on (GemmArgs::pos_adv), so the
 // id belongs at pos - 1 and the position stays
 __device__ __forceinline__ void argmax_finish(float best, int bi, int32_t* __restrict__ out,
-                                              DecState* __restrict__ st, int hist_off = 0) {
+                                              DecState* __restrict__ st, int hist_off = 0, int n_ids = 0) {
     constexpr int NT = 1024;
     const int tid = threadIdx.x;
     group_argmax<64>(best, bi, tid & 63);
@@ -42,6 +42,7 @@ __device__ __forceinline__ void argmax_finish(float best, int bi, int32_t* __res
         bi = tid < NT / 64 ? si[tid] : 0x7fffffff;
         group_argmax<16>(best, bi, tid);  // the NT / 64 = 16 wave results in lanes 0-15
         if (tid == 0) {
+            if (n_ids > 0) L3_DCHECK(bi >= 0 && bi < n_ids, CHK_TOKEN_ID);
             out[blockIdx.x] = bi;
             if (st) {
                 // captured decode step: record the id in the generate history, and the last row
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const float* __restrict__ 
         for (int i = tid; i < n; i += NT)
             if (argmax_better(row[i], i, best, bi)) { best = row[i]; bi = i; }
     }
-    argmax_finish(best, bi, out, st);
+    argmax_finish(best, bi, out, st, 0, n);
 }
 
 // one row from the batch-1 lm_head's per-block (value, index) partials (GemmArgs::amax_part):
@@ -252,6 +253,7 @@ __global__ void kv_restore_kernel(float* cache, const float* bak, int B, int KVH
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B * KVH * HD) return;
     const int d = i % HD, bh = i / HD;  // bh = b * KVH + h
+    if (i == 0) L3_DCHECK(pos >= 0 && pos < Smax, CHK_KV_SLOT);
     cache[((int64_t)bh * Smax + pos) * HD + d] = bak[i];
 }
 
@@ -263,5 +265,19 @@ hipError_t launch_kv_restore(float* cache, const float* bak, int B, int KVH, int
                        Smax, HD, pos);
     return hipGetLastError();
 }
+
+// device bounds checks (kernels.h): a check build's self-test — one violation of each class
+// recorded, so a caller can see the counters reach the host
+__global__ void dcheck_selftest_kernel(int n) {
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        for (int c = 0; c < n; ++c) L3_DCHECK(false, c);
+}
+
+hipError_t launch_dcheck_selftest(hipStream_t s) {
+    hipLaunchKernelGGL(dcheck_selftest_kernel, dim3(1), dim3(64), 0, s, (int)CHK_TOKEN_ID + 1);
+    return hipGetLastError();
+}
+
+hipError_t dcheck_collect_misc(unsigned* out) { return dcheck_collect(out); }
 
 }  // namespace l3

@@ -1908,6 +1908,31 @@ extern "C" int l3_decode_recoveries(l3_ctx* c, int64_t* count) {
     return 0;
 }
 
+// device bounds checks (kernels.h L3_DCHECK): the counts every kernel of this library
+// recorded on the context's device since the last call, then cleared (a check build only)
+extern "C" int l3_device_check_counts(l3_ctx* c, uint32_t* counts, int32_t* enabled) {
+    CHECK_CTX(c);
+    if (enabled) *enabled = L3_DCHECK_ON;
+    if (!counts) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned n[CHK_N] = {};
+    HIP_TRY(dcheck_collect_gemm(n));
+    HIP_TRY(dcheck_collect_attention(n));
+    HIP_TRY(dcheck_collect_misc(n));
+    HIP_TRY(dcheck_collect_persist(n));
+    for (int i = 0; i < CHK_N; ++i) counts[i] = n[i];
+    return 0;
+}
+
+extern "C" int l3_device_check_selftest(l3_ctx* c) {
+    CHECK_CTX(c);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_dcheck_selftest(c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 extern "C" int l3_decode_stats(l3_ctx* c, int64_t* graph_steps, int64_t* speculative_hits) {
     CHECK_CTX(c);
     if (graph_steps) *graph_steps = c->graph_steps;

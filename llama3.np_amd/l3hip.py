@@ -102,6 +102,8 @@ _SIGNATURES = {
     "l3_group_forward_dev": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
     "l3_group_greedy_step_host": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _P]),
     "l3_group_synchronize": (ctypes.c_int, [_P]),
+    "l3_device_check_counts": (ctypes.c_int, [_P, _P, _P]),
+    "l3_device_check_selftest": (ctypes.c_int, [_P]),
 }
 
 BUSID_LEN = 16  # L3_BUSID_LEN
@@ -394,6 +396,18 @@ class Context:
         v = ctypes.c_int64(0)
         check(lib().l3_decode_recoveries(self._h, ctypes.byref(v)))
         return int(v.value)
+
+    def device_check_counts(self):
+        """(enabled, counts): the device bounds-check counters (check build, L3_LIB_PATH =
+        libllama3hip_check.so) since the last call — K / V slot, attention keys, token id."""
+        n = np.zeros(4, np.uint32)
+        en = ctypes.c_int32(0)
+        check(lib().l3_device_check_counts(self._h, n.ctypes.data_as(ctypes.c_void_p), ctypes.byref(en)))
+        return bool(en.value), {"kv_slot": int(n[0]), "attn_keys": int(n[1]), "token_id": int(n[2])}
+
+    def device_check_selftest(self) -> None:
+        """One recorded violation of each check class (check build; a no-op in the release one)."""
+        check(lib().l3_device_check_selftest(self._h))
 
     def decode_stats(self) -> dict:
         """Decode steps served by graph replay, and of those by a speculative step."""
