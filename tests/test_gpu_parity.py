@@ -635,6 +635,30 @@ def test_decode_shrinking_batches_against_oracle(tmpdir_mod):
     np.testing.assert_array_equal(m.generate_all(prompt, 30), orc.greedy_ids(ref, prompt, 30))
 
 
+def test_decode_past_256_rows_against_oracle(tmpdir_mod):
+    """Batched decode with more rows than the skinny kernel takes (B = 300: the L = 1 layer GEMMs
+    on the tiled MFMA kernel, the decode attention over 300 x 6 workgroups): eager steps' logits
+    against the oracle on the default-scale weights (the north star's 1e-4 bar; the sharp set's
+    near-zero logits among 300 x 32000 sit at that bar's edge in fp32, 9 of 9.6M at 1.0-1.8e-4),
+    and the device loop's ids on the sharp set (llama3.py:163-211, 304-321)."""
+    args = synth.stories15m(300)
+    args.max_seq_len = 64
+    rng = np.random.default_rng(10)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 9, "default")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    ids = rng.integers(0, args.vocab_size, (300, 8))
+    _close(m(ids, 0), ref(ids, 0))
+    for pos in (8, 9, 10):
+        nxt = rng.integers(0, args.vocab_size, (300, 1))
+        _close(m(nxt, pos), ref(nxt, pos))
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 9, "sharp")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    prompt = rng.integers(0, args.vocab_size, (300, 5))
+    np.testing.assert_array_equal(m.generate_all(prompt, 16), orc.greedy_ids(ref, prompt, 16))
+
+
 @pytest.mark.parametrize("dim,heads,kv_heads", [(512, 4, 1), (128, 4, 2), (192, 2, 1)])
 def test_head_dims_gqa_decode_with_norm_weights(tmpdir_mod, dim, heads, kv_heads):
     """Head geometries beyond stories15M's 48 — HD = 128 (Llama-3, n_rep = 4), 32 and 96 — with
