@@ -281,6 +281,27 @@ def test_full_size_batch_rows_independent_and_match_oracle(tmpdir_mod):
     assert _close(full[rows], ref(ids[rows], 0)) <= 1e-4
 
 
+def test_full_size_chunked_prefill_equals_whole(tmpdir_mod):
+    """At the benchmark shape (B = 256), the prompt prefilled in chunks — 100 tokens, then 156
+    at start_pos 100 (llama3.py:293-297's zero-prefix mask, the cache read back) — ends at the
+    same last-position logits as the whole 256-token prefill, and a decode step after either
+    gives the same logits: a size-independent property of the causal cache (fp32 rounding bar:
+    the chunks' GEMMs and attention tiles group the rows differently)."""
+    args = synth.stories15m(256)
+    args.max_seq_len = 264  # room for the decode step after the 256-token prompt
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    m = llama3.Llama(path, args)
+    rng = np.random.default_rng(21)
+    ids = rng.integers(0, args.vocab_size, (256, 256))
+    nxt = rng.integers(0, args.vocab_size, (256, 1))
+    whole = np.array(m(ids, 0), copy=True)
+    step_whole = np.array(m(nxt, 256), copy=True)
+    m(ids[:, :100], 0)
+    chunked = m(ids[:, 100:], 100)
+    np.testing.assert_allclose(chunked, whole, rtol=0, atol=2e-5)
+    np.testing.assert_allclose(m(nxt, 256), step_whole, rtol=0, atol=2e-5)
+
+
 @pytest.mark.parametrize("B", [63, 160])
 def test_batch_split_bit_identical(tmpdir_mod, B):
     """The batch split (row ranges on concurrent streams, l3_set_batch_split) changes only
