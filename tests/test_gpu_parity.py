@@ -284,8 +284,8 @@ def test_full_size_batch_rows_independent_and_match_oracle(tmpdir_mod):
 def test_full_size_chunked_prefill_equals_whole(tmpdir_mod):
     """At the benchmark shape (B = 256), the prompt prefilled in chunks — 100 tokens, then 156
     at start_pos 100 (llama3.py:293-297's zero-prefix mask, the cache read back) — ends at the
-    same last-position logits as the whole 256-token prefill, and a decode step after either
-    gives the same logits: a size-independent property of the causal cache (fp32 rounding bar:
+    same last-position logits as the whole 256-token prefill, a decode step after either gives
+    the same logits, and those are the last position of one 257-token prefill: a size-independent property of the causal cache (fp32 rounding bar:
     the chunks' GEMMs and attention tiles group the rows differently)."""
     args = synth.stories15m(256)
     args.max_seq_len = 264  # room for the decode step after the 256-token prompt
@@ -300,6 +300,8 @@ def test_full_size_chunked_prefill_equals_whole(tmpdir_mod):
     chunked = m(ids[:, 100:], 100)
     np.testing.assert_allclose(chunked, whole, rtol=0, atol=2e-5)
     np.testing.assert_allclose(m(nxt, 256), step_whole, rtol=0, atol=2e-5)
+    # and the decode step's logits are the last position of one 257-token prefill
+    np.testing.assert_allclose(m(np.concatenate([ids, nxt], axis=1), 0), step_whole, rtol=0, atol=2e-5)
 
 
 @pytest.mark.parametrize("B", [63, 160])
