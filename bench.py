@@ -297,8 +297,8 @@ def cpu_baseline():
                       f"(affinity {affinity}; cap: {cap or 'none'})"}
 
 
-def traffic_per_launch(rows):
-    p = os.path.join(REPO, "profiles", "pmc_gateup.json")
+def traffic_per_launch(rows, name="pmc_gateup.json"):
+    p = os.path.join(REPO, "profiles", name)
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -461,7 +461,8 @@ def bench_c5(a):
         "whole_forward_frac": round(total * a.steps / el / 1e12 / PEAK_FP32_TFLOPS, 4),
         "roofline": {"kernel": "gemm gate|up, M=131072 K=4096 N=28672", "bound": "mfma",
                      "achieved": gu, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(gu / PEAK_FP32_TFLOPS, 4), "traffic": None},
+                     "frac": round(gu / PEAK_FP32_TFLOPS, 4),
+                     "traffic": traffic_per_launch(T, "pmc_c5_gateup.json")},
         "kernels": per, "weight_upload_s": round(t_up, 1),
         "output_check": {"all_finite": finite, "row0_vs_B1_run_max_abs": row_err, "tol": "1e-5 abs+rel"},
         "lib": {"version": l3hip.version(), "source_hash": l3hip.source_hash()}}))

@@ -261,10 +261,18 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     // Configurations chosen with tools/gemm_tune (interleaved A/B on MI355X).
     // 128 x 128 BK16: 120 VGPRs + 32 KB LDS -> 4 blocks per CU.
     const bool small_m = a.M <= 32;  // tiny M: 16 x 128 tile
+    // long K (the Llama-3 shape's gate|up): tiles in groups of 8 row tiles, so a k-step's
+    // concurrent blocks on an XCD share 8 A slices and ~12 W slices in L2 instead of one A slice
+    // and ~96 W slices (C5 gate|up 134.7 -> 135.8 TF/s, whole forward +0.3 %, bit-identical,
+    // profiles/r05_gemm_group_ab.txt; QKV -0.3 % and C3's K = 288 -0.4 % keep the row-major
+    // order); L3_GEMM_GROUP_M=0 turns it off (A/B)
+    static const int group_env = env_knob("L3_GEMM_GROUP_M", 8);
+    GemmArgs ag = a;
+    ag.group_m = a.K >= 1024 && !small_m ? group_env : 0;
     switch (epi) {
         case EPI_SWIGLU:  // 128 x 128, BK 16
             if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2, 32>(a, s);
-            return launch<EPI_SWIGLU, 2, 2, 4, 4, 3, 16>(a, s);
+            return launch<EPI_SWIGLU, 2, 2, 4, 4, 3, 16>(ag, s);
         case EPI_QKV:     // 128 x 96 at short K (stories15M), else 128 x 128; BK 16
             if (small_m) return launch<EPI_QKV, 1, 4, 1, 2, 2, 32>(a, s);
             if (a.N % 96 == 0 && a.K <= 1024) return launch<EPI_QKV, 2, 2, 4, 3, 4, 16>(a, s);

@@ -392,7 +392,15 @@ __global__ void __launch_bounds__(64 * WM * WN, WAVES_PER_EU) gemm_lds_kernel(Ge
     const int ntiles = SPLIT ? ((p.M + BM - 1) / BM) * ntn : 1;
     const int ks = SPLIT ? tb / ntiles : 0;      // k-slice
     const int t = SPLIT ? tb - ks * ntiles : tb;  // tile
-    const int m0 = (t / ntn) * BM, n0 = (t % ntn) * BN;
+    int mt = t / ntn, nt = t - mt * ntn;
+    if (p.group_m > 1) {  // GemmArgs::group_m: group of group_m row tiles, column-major inside
+        const int ntm = (p.M + BM - 1) / BM;
+        const int g = t / (p.group_m * ntn), first = g * p.group_m;
+        const int gm = min(ntm - first, p.group_m), local = t - g * p.group_m * ntn;
+        mt = first + local % gm;
+        nt = local / gm;
+    }
+    const int m0 = mt * BM, n0 = nt * BN;
     const int nk = SPLIT ? p.K / BK / p.splits : p.K / BK;  // k-tiles of this block
     const int kb = ks * nk * BK;                           // its first k
     unsigned long long stamps[8];

@@ -18,7 +18,7 @@ namespace l3 {
 //                L3_DECODE_PERSIST_STAMPS=<file> (diagnostic timeline, tools/persist_stamps.py)
 //   gemm.hip     L3_SPLITK (1), L3_SPLITK_CFG (0), L3_SPLITK_BLOCKS (1024), L3_SPLITK_MINKT (8),
 //                L3_GEMV_NT (1), L3_GEMV_LPU (0 = by shape), L3_GEMV_MR (by shape), L3_SKINNY (1),
-//                L3_SKINNY_MIN (9), L3_SKINNY_CH (2), L3_SKINNY_TN2_MIN (256)
+//                L3_SKINNY_MIN (9), L3_SKINNY_CH (2), L3_SKINNY_TN2_MIN (256), L3_GEMM_GROUP_M (8)
 inline int env_knob(const char* name, int def) {
     const char* e = getenv(name);
     return e && *e ? atoi(e) : def;
@@ -136,6 +136,10 @@ struct GemmArgs {
     // the skinny MFMA kernel whatever M and W (a pruned last layer: every row rounds the same
     // way for any batch split, runtime.hip run_layer last_rows)
     bool force_skinny;
+    // tiled kernel: tile order within each XCD's run of tiles — 0 row-major (n fastest), g > 0
+    // groups of g row tiles walked column by column, so a k-step's concurrent blocks share g A
+    // slices and ~blocks / g W slices in L2 (set by launch_gemm for long K; results identical)
+    int group_m;
 };
 constexpr int GEMV_MAXP = 8;
 constexpr int KV_BAK_SLOTS = 32;  // > the decode steps ever run ahead (runtime.hip SPEC_AHEAD)

@@ -54,6 +54,15 @@ struct Variant {
                 const int64_t blocks = (int64_t)((a.M + 15) / 16) * ((a.N + 16 * TN - 1) / (16 * TN)); \
                 hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, CH, NW>), dim3((unsigned)blocks), dim3(64 * NW), 0, s, a); \
             }}
+// the product tile with GemmArgs::group_m = G (grouped tile order inside each XCD's run)
+#define GVARG(WM, WN, TM, TN, EPI, WPE, BK, G)                                                       \
+    Variant{"glds<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ",bk" #BK ",gm" #G ">", [](const GemmArgs& a0, hipStream_t s) { \
+                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                  \
+                GemmArgs a = a0;                                                                     \
+                a.group_m = G;                                                                       \
+                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);        \
+                hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true>), dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a); \
+            }}
 #define RVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("regs", false, WM, WN, TM, TN, EPI, WPE, BK)
 #define GVAR(WM, WN, TM, TN, EPI, WPE, BK) TVAR("glds", true, WM, WN, TM, TN, EPI, WPE, BK)
 
@@ -344,6 +353,21 @@ int main(int argc, char** argv) {
                            : std::vector<Variant>{SVARW(EPI_RESID, 1, 2, 4), SVARW(EPI_RESID, 1, 2, 2), SVARW(EPI_RESID, 1, 2, 8), SVARW(EPI_RESID, 1, 1, 8)},
                       rounds, iters);
         }
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "group") {  // round 5: grouped tile order, C5 and C3 shapes
+        const int Mc = 16384;
+        run_shape("C5 gate|up", EPI_SWIGLU, Mc, 4096, 28672, true,
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVARG(2, 2, 4, 4, EPI_SWIGLU, 3, 16, 4),
+                   GVARG(2, 2, 4, 4, EPI_SWIGLU, 3, 16, 8), GVARG(2, 2, 4, 4, EPI_SWIGLU, 3, 16, 16)}, rounds, 3);
+        run_shape("C5 QKV-shape (store)", EPI_STORE, Mc, 4096, 6144, true,
+                  {GVAR(2, 2, 4, 4, EPI_STORE, 3, 16), GVARG(2, 2, 4, 4, EPI_STORE, 3, 16, 8)}, rounds, 3);
+        run_shape("C5 O-proj", EPI_RESID, Mc, 4096, 4096, false,
+                  {GVAR(2, 2, 4, 4, EPI_RESID, 2, 32), GVARG(2, 2, 4, 4, EPI_RESID, 2, 32, 8)}, rounds, 3);
+        run_shape("C5 down", EPI_RESID, Mc, 14336, 4096, false,
+                  {GVAR(2, 2, 4, 4, EPI_RESID, 2, 32), GVARG(2, 2, 4, 4, EPI_RESID, 2, 32, 8)}, rounds, 3);
+        run_shape("C3 gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true,
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), GVARG(2, 2, 4, 4, EPI_SWIGLU, 3, 16, 8)}, rounds, iters);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "big8") {  // round 5: 8-wave blocks at the C3 shapes

@@ -26,6 +26,8 @@ for s in "$@"; do
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 ;;
+    pmcc5) step pmc_c5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_c5_fetch -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1
+         step pmc_c5_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_c5_write -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1 ;;
     tune) step tune 600 tools/gemm_tune 5 10 ;;
     tunerows) step tunerows 600 tools/gemm_tune 5 10 rows ;;
     tunering) step tunering 600 tools/gemm_tune 5 10 ring ;;

@@ -1,6 +1,9 @@
 """HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
 
     python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/pmc_gateup.json <source_hash>
+    python tools/pmc_traffic.py gpurun_out/pmc_c5_fetch gpurun_out/pmc_c5_write profiles/pmc_c5_gateup.json <source_hash> c5
+
+(the second form: the Llama-3-shape prefill, bench.py --workload c5, B=64 x L=2048 rows)
 
 <source_hash> is `l3_source_hash()` of the library the passes ran (printed in every bench
 line as lib.source_hash); bench.py reports `traffic` only while the library it loads has it.
@@ -49,7 +52,11 @@ def calibrated(kernel: str) -> bool:
 
 
 def main():
+    global ROWS, D, FD
     fetch_dir, write_dir, out = sys.argv[1:4]
+    c5 = len(sys.argv) > 5 and sys.argv[5] == "c5"
+    if c5:
+        ROWS, D, FD = 64 * 2048, 4096, 14336
     fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     kernels = {}
     for k in fe:
@@ -65,8 +72,9 @@ def main():
     # the gate|up GEMM is the gemm kernel instantiated with EPI_SWIGLU (5th template argument 2)
     gu = [k for k in kernels if re.search(r"gemm_\w+_kernel<\d+, \d+, \d+, \d+, 2[,>]", k)]
     algo = 4 * (ROWS * D + 2 * FD * D + ROWS * FD)
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, "
-                     "python bench.py --steps 2 --warmup 1 --split 1 (every launch full size)",
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, " +
+                     ("python bench.py --workload c5 --layers 2 --steps 1 --warmup 1" if c5 else
+                      "python bench.py --steps 2 --warmup 1 --split 1 (every launch full size)"),
            "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE half-count) for "
                          "the 16-B/lane coalesced streaming kernels only; others uncalibrated (range)",
            "workload_rows": ROWS,
