@@ -1,5 +1,7 @@
 # Interleaved A/B: the committed library (tools/variants/libllama3hip_r5.so) against the tree with
 # the multi-step persistent launch off / on (L3_DECODE_PERSIST_MULTI), tools/bench_decode.py.
+# (L3_DECODE_PERSIST_MULTI exists only in the research build: tools/research/decode_persist_multistep.hip
+# in place of llama3.np_amd/csrc/decode_persist.hip; the product library ignores it)
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
