@@ -286,6 +286,10 @@ def cpu_baseline():
     return {"value": round(Bs * SEQ / t, 1), "unit": "tokens/s", "cores": int(blas), "threads": int(blas),
             "nproc": os.cpu_count(), "affinity": affinity, "openblas_threads": int(blas),
             "thread_cap": cap,
+            "cores_why": ("all the cores this job may use: the GPU box gives one GPU's job a 16-CPU share "
+                          "(it exports OMP_NUM_THREADS=16 and its rules size worker pools to that share); "
+                          "nproc / affinity report the whole host, not the share") if cap and cap.endswith("=16")
+                         else "OpenBLAS's own thread count on this host",
             "value_1_thread_sample": one,
             "sample_1_thread": f"B={B1} of the C3 batch's {Bs} rows, L={SEQ}, one forward, "
                                f"OpenBLAS limited to 1 thread (rows independent: same per-row work)",
@@ -295,6 +299,35 @@ def cpu_baseline():
                       f"1 warm-up, median of 3 ({', '.join(f'{x:.2f}' for x in times)} s), "
                       f"OpenBLAS threads={blas} of nproc={os.cpu_count()} "
                       f"(affinity {affinity}; cap: {cap or 'none'})"}
+
+
+def step_flops(args, FD, B, L, pruned):
+    """Algorithmic FLOPs one forward executes (SURVEY 8(d) counts; llama3.py:166-211,97-103,304-307).
+
+    pruned=False: every row through every layer (GEMMs 2*T*K*N each, causal attention
+    4*H*HD*B*L(L+1)/2) + the last-position lm_head.  pruned=True: what the product forward runs
+    (runtime.hip run_layer(..., last_rows)): the last block computes K / V for every position (the
+    cache) and its q, attention (one query per sequence over L keys), O-proj and FFN on each
+    sequence's last position only.  C3: 845.68 GFLOP all rows, 727.8 pruned."""
+    D, H = args.dim, args.n_heads
+    KVH = args.n_kv_heads or H
+    HD = D // H
+    qdim, kvdim = H * HD, KVH * HD
+    T = B * L
+
+    def gemms(rows, qkv_cols):
+        return 2.0 * rows * D * (qkv_cols + qdim + 3 * FD) if qkv_cols else 0.0
+
+    full = gemms(T, qdim + 2 * kvdim) + 4.0 * H * HD * B * L * (L + 1) / 2
+    lm = 2.0 * B * D * args.vocab_size
+    nl = args.n_layers
+    if not pruned or L == 1 or nl < 2:
+        return nl * full + lm
+    last = (2.0 * T * D * 2 * kvdim            # K / V of every position
+            + 2.0 * B * D * qdim               # q of the last positions
+            + 4.0 * H * HD * B * L             # one query per sequence over L keys
+            + 2.0 * B * D * (qdim + 3 * FD))   # O-proj, gate|up, down on B rows
+    return (nl - 1) * full + last + lm
 
 
 def traffic_per_launch(rows, name="pmc_gateup.json"):
@@ -779,6 +812,19 @@ def main():
     ffn_tf = (gu_flops + dn_flops) / ((gu_ms / gu_n + dn_ms / dn_n) / 1e3) / 1e12
     traffic = traffic_per_launch(T)
     host_ms = elapsed_d2h / d2h_steps * 1e3
+    # the whole step against the MFMA peak: the FLOPs the timed (pruned) step executes over its
+    # wall time, and the all-rows step's full algorithmic count over its own time
+    fl_pruned = step_flops(args, FD, bpg, SEQ, True)
+    fl_all = step_flops(args, FD, bpg, SEQ, False)
+    tf_step = fl_pruned * a.steps / elapsed / 1e12
+    tf_all = fl_all * a.steps / elapsed_all_rows / 1e12
+    whole_step = {"executed_gflop": round(fl_pruned / 1e9, 2), "achieved": round(tf_step, 2),
+                  "frac": round(tf_step / PEAK_FP32_TFLOPS, 4),
+                  "all_rows": {"gflop": round(fl_all / 1e9, 2), "achieved": round(tf_all, 2),
+                               "frac": round(tf_all / PEAK_FP32_TFLOPS, 4)},
+                  "unit": "TFLOP/s", "peak": PEAK_FP32_TFLOPS,
+                  "note": "per GPU; executed = the timed step's own work (last block on each sequence's "
+                          "last position, step_flops in bench.py), wall clock of the same steps as value"}
     out = {
         "metric": METRIC,
         "value": round(tokens / elapsed, 1),
@@ -813,6 +859,7 @@ def main():
                    "parallelism": f"dp{dist.world} (batch rows) + RCCL logits gather"},
         "lib": {"version": l3hip.version(), "source_hash": l3hip.source_hash()},
         **(dist.info or {}),
+        "whole_step": whole_step,
         "roofline": {"kernel": f"gemm gate|up (fused SwiGLU epilogue), M={T} K=288 N=1536",
                      "pass": "same workload and step count, batch split off (HIP events need "
                              "the kernel alone on the CUs)",

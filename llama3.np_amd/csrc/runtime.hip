@@ -1164,7 +1164,11 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
             a.kv_bak = c->bak_capture ? c->kv_bak : nullptr;
             a.from_parts = i > 0;            // the previous step in this graph left partials only
             a.write_id = i == steps - 1;     // the last one publishes the id for the host / next graph
-            a.fault_pos = env_knob("L3_DECODE_PERSIST_FAULT", -1);  // test knobs (kernels.h)
+            // test-only fault injection (kernels.h): honoured only together with
+            // L3_TEST_FAULT_INJECTION=1, so a stray L3_DECODE_PERSIST_FAULT in a user's
+            // environment cannot fail a step and switch the context to the graph path
+            const bool inject_ok = env_knob("L3_TEST_FAULT_INJECTION", 0) == 1;
+            a.fault_pos = inject_ok ? env_knob("L3_DECODE_PERSIST_FAULT", -1) : -1;
             a.fault_wg = env_knob("L3_DECODE_PERSIST_FAULT_WG", 1);
             refused = launch_decode_persist(a, pgrid, c->stream) != hipSuccess;
         }

@@ -110,6 +110,7 @@ def test_persistent_decode_fault_recovers_device_loop(tmpdir_mod, monkeypatch, f
     g, args, path = _stories(tmpdir_mod, "sharp")
     prompt, want, n = _dream(g)
     monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    monkeypatch.setenv("L3_TEST_FAULT_INJECTION", "1")
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", str(fault_pos))
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
     m = llama3.Llama(path, args)
@@ -135,6 +136,7 @@ def test_persistent_decode_fault_recovers_lazy(tmpdir_mod, monkeypatch, fault_po
     g, args, path = _stories(tmpdir_mod, "sharp")
     prompt, want, n = _dream(g)
     monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    monkeypatch.setenv("L3_TEST_FAULT_INJECTION", "1")
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", str(fault_pos))
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
     m = llama3.Llama(path, args)
@@ -157,6 +159,7 @@ def test_persistent_decode_fault_in_abandoned_run_ahead(tmpdir_mod, monkeypatch)
     g, args, path = _stories(tmpdir_mod, "sharp")
     prompt, want, n = _dream(g)
     monkeypatch.setenv("L3_DECODE_PERSIST", "1")
+    monkeypatch.setenv("L3_TEST_FAULT_INJECTION", "1")
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", "20")
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", "255")
     m = llama3.Llama(path, args)

@@ -661,9 +661,12 @@ def test_decode_shrinking_batches_against_oracle(tmpdir_mod):
 def test_decode_past_256_rows_against_oracle(tmpdir_mod):
     """Batched decode with more rows than the skinny kernel takes (B = 300: the L = 1 layer GEMMs
     on the tiled MFMA kernel, the decode attention over 300 x 6 workgroups): eager steps' logits
-    against the oracle on the default-scale weights (the north star's 1e-4 bar; the sharp set's
-    near-zero logits among 300 x 32000 sit at that bar's edge in fp32, 9 of 9.6M at 1.0-1.8e-4),
-    and the device loop's ids on the sharp set (llama3.py:163-211, 304-321)."""
+    against the oracle on the default-scale weights (the north star's 1e-4 bar), and the device
+    loop's ids on the sharp set (llama3.py:163-211, 304-321).  The sharp set's logits are not held
+    to the plain 1e-4 here: on it 9 of the 9.6M logits differ from the oracle by 1.0-1.8e-4, the
+    worst 1.84e-4 at a reference logit of -7.77 (gpurun_out/diag_b300.log, round 5) -- inside the
+    reference suite's own atol 1e-4 + rtol 2e-4 form (tests/test_llama_implementations.py:23-24),
+    outside the north star's plain 1e-4, so that set is checked through its greedy ids."""
     args = synth.stories15m(300)
     args.max_seq_len = 64
     rng = np.random.default_rng(10)
