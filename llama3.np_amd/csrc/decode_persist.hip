@@ -33,8 +33,11 @@
 // the 25-kernel graph path).  A layer workgroup keeps the K / V rows its stage A computes (and,
 // for the run-ahead undo, the slots' previous contents) in LDS and writes them to the caches only
 // after its last wait of the step, which every layer workgroup passes exactly when every stage of
-// every layer has published; workgroup 0 records that point (epoch[2] = pos + 1), so after a
-// failure the host knows whether the step's slots were written (all of them) or not (none).
+// every layer has published, and then stores its write mark (the launch's tag); a workgroup that
+// gives up records the failing launch's tag in epoch[2].  After a failure the undo
+// (kv_restore_kernel, KvGuard) therefore restores exactly the units whose workgroup's mark equals
+// that tag — all of them, none, or (a hand-off arriving at the edge of one workgroup's ~1 s bound)
+// some — and never a slot the failed launch did not write.
 //
 // Work split (grid = 256 workgroups x 256 threads, all resident: 1 per CU by resources, checked
 // against the device by decode_persist_grid before a capture): the layer stages run on workgroups
@@ -83,6 +86,7 @@ struct Ctx {
 // waiting gives up at its next check, every later launch returns at once)
 __device__ __forceinline__ void give_up(const Ctx& c) {
     *c.bad = 1;
+    __hip_atomic_store(c.p.epoch + 2, c.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the failing launch
     __hip_atomic_store(c.p.err, (unsigned)c.pos + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(c.p.epoch + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -135,7 +139,7 @@ __device__ __forceinline__ bool sweep_n(const Ctx& c, u64* g, int n, float* dst,
     if (n <= NT) return sweep<1>(c, g, n, dst, idx, sleep, stick, nst);
     if (n <= 2 * NT) return sweep<2>(c, g, n, dst, idx, sleep, stick, nst);
     if (n <= 4 * NT) return sweep<4>(c, g, n, dst, idx, sleep, stick, nst);
-    return sweep<5>(c, g, n, dst, idx, sleep, stick, nst);  // n <= 1280: FD (<= 1024) + the start marks
+    return sweep<5>(c, g, n, dst, idx, sleep, stick, nst);  // n <= 1280
 }
 
 // block max / sum of one value per thread (every thread gets it), one barrier each: the two use
@@ -257,7 +261,8 @@ __device__ __forceinline__ int stage_unit(const DecodePersistArgs& p, int n, int
 }  // namespace persist
 
 // One launch = one decode step.  Granule slab per layer: [qkv | o | h1 | hid | h2]
-// (decode_persist_slab), then the lm_head partials [2 * 256], then the start marks [256].
+// (decode_persist_slab), then the lm_head partials [2 * 256], the start marks [256] and the layer
+// workgroups' write marks [GL] (32-bit, in a 256-granule block).
 // NCD / NCF: float4 per lane of a W row with K = D / K = FD (>= ceil(K / 64)); KPF >= HD / 4 (the
 // old keys' chunks each attention lane holds); LMPF: lm_head passes of 16 rows each workgroup
 // holds in registers.
@@ -284,6 +289,7 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     const int64_t slab = decode_persist_slab(H, KVH, HD, D, FD);
     u64* lm_g = p.gran + slab * p.n_layers;
     u64* marks = lm_g + 2 * 256;
+    unsigned* wmarks = reinterpret_cast<unsigned*>(marks + 256);
     // start mark: this workgroup has read the launch's tag (workgroup 0 moves the epoch on only
     // after seeing every mark, so no workgroup dispatched late can read the next launch's tag)
     if (tid == 0) gput(marks + wg, tag, 0.f);
@@ -296,7 +302,10 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
     // test knob (L3_DECODE_PERSIST_FAULT): workgroup fault_wg gives up at once in the step at
     // fault_pos (a layer workgroup after reducing the previous step's partials, as every layer
     // workgroup does before its first wait: the previous step's id always reaches the history)
-    const bool fault = pos == p.fault_pos && wg == p.fault_wg;
+    // fault_late: a layer workgroup gives up at its last wait instead (stage E of the last layer,
+    // every stage before it published: the other layer workgroups pass and write their slots)
+    const bool fault_late = pos == p.fault_pos && wg == p.fault_wg && p.fault_late;
+    const bool fault = pos == p.fault_pos && wg == p.fault_wg && !fault_late;
     const int64_t h2_off = (int64_t)qkvn + qdim + D + FD;  // h2 within a slab
     const int K4d = D / 4, K4f = FD / 4, K4q = qdim / 4;
     // roles: layer workgroup (the layer stages; the attention of head wg < H) or lm workgroup lwg
@@ -659,13 +668,11 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
             const int row[1] = {u};
             f32x4 w[1][NCF];
             load_rows<1, NCF>(p.wd[li], row, K4f, w);
-            // workgroup 0's last wait also covers every workgroup's start mark (they were written
-            // at launch: no extra round trip for the check the epoch bump needs)
-            const bool last0 = wg == 0 && li + 1 == p.n_layers;
-            const int64_t mk = marks - g_hid;
-            if (!sweep_n(c, g_hid, last0 ? FD + G : FD, xs, [=](int i) { return i < FD ? (int64_t)i : mk + (i - FD); }, 1,
-                         false, FD))
+            if (fault_late && li + 1 == p.n_layers) {
+                if (tid == 0) give_up(c);
                 return;
+            }
+            if (!sweep_n(c, g_hid, FD, xs, [](int i) { return i; })) return;
             stamp(9 + 10 * li);
             float acc[1];
             dot_rows<1, NCF>(w, xs, K4f, acc);
@@ -695,13 +702,18 @@ __global__ void __launch_bounds__(256, 1) decode_persist_kernel(DecodePersistArg
                 *reinterpret_cast<float2*>(cache[li] + coff) = float2{e.x, e.y};
             }
         }
+        // this workgroup's write mark: every one of its threads is past the last wait (the sweep
+        // ends in a barrier with no give-up), so each stores its slots above — nothing can stop it
+        // between that barrier and here
+        if (tid == 0) __hip_atomic_store(wmarks + wg, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (wg != 0) return;
-    // ---- workgroup 0: its last wait saw the whole chain (so every layer workgroup writes its
-    // slots) and every workgroup's start mark (every one has read this launch's tag: an lm
-    // workgroup dispatched late — another kernel holding its CU — would otherwise read the moved
-    // epoch and wait for granules no launch writes) ---------------------------------------------
-    if (tid == 0) __hip_atomic_store(p.epoch + 2, (unsigned)pos + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // ---- workgroup 0, its own slots written: every workgroup's start mark (every one has read this
+    // launch's tag — an lm workgroup dispatched late, another kernel holding its CU, would
+    // otherwise read the moved epoch and wait for granules no launch writes) before the epoch
+    // moves on.  Waited for after the slot writes, so a give-up here (a workgroup never
+    // dispatched) leaves this workgroup's mark set and its slots restorable (kv_bak) ------------
+    if (!sweep_n(c, marks, G, xs, [](int i) { return i; }, 1, false, 0)) return;
     if (!p.write_id) {
         // the next launch reduces this step's partials itself; only the position moves on here
         // (every layer workgroup read it at its start: none could have finished layer 0 else)

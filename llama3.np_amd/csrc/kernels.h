@@ -323,6 +323,7 @@ struct DecodePersistArgs {
     unsigned* err;                 // host-mapped: pos + 1 of the step in which a workgroup gave up
     unsigned long long* stamps;    // diagnostic (null): [workgroup][128] s_memrealtime at stage points
     int fault_pos, fault_wg;       // test knob: workgroup fault_wg gives up in the step at fault_pos (-1: none)
+    int fault_late;                // ... at its last wait of the step instead of its first (a layer workgroup)
 };
 // granules per layer of the persistent step: [qkv | o | h1 | hid | h2]
 __host__ __device__ inline int64_t decode_persist_slab(int H, int KVH, int HD, int D, int FD) {
@@ -360,8 +361,17 @@ hipError_t launch_rmsnorm(const float* x, const float* w, float* y, int64_t rows
                           float eps, hipStream_t s);
 hipError_t launch_fold_cols(float* W, int64_t rows, int K, const float* w, hipStream_t s);
 // cache[b][h][pos][:] = bak[b][h][:] for b < B, h < KVH (undo of a speculative decode step)
+// the persistent step's failure words, read by the undo on the device (kv_restore_kernel); err
+// null: restore unconditionally (the graph path's steps cannot fail)
+struct KvGuard {
+    const unsigned* err;     // host-mapped error word: failed position + 1, or 0
+    const unsigned* epoch;   // [3]; epoch[2]: the tag of the launch that gave up
+    const unsigned* wmarks;  // [GL] each layer workgroup's write mark (the tag of its last write)
+    int col_base;            // QKV column of this cache's first element (qdim, or qdim + kvdim)
+    int per;                 // RoPE-pair units per layer workgroup (stage_unit: ceil(qkvn / 2 / GL))
+};
 hipError_t launch_kv_restore(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos,
-                             hipStream_t s);
+                             hipStream_t s, KvGuard g = KvGuard{});
 // device bounds-check counters of each translation unit (L3_DEVICE_CHECKS builds; else no-ops)
 hipError_t dcheck_collect_gemm(unsigned* out);
 hipError_t dcheck_collect_attention(unsigned* out);

@@ -249,20 +249,37 @@ hipError_t launch_fold_cols(float* W, int64_t rows, int K, const float* w, hipSt
 }
 
 // undo of a speculative decode step's K / V append (runtime.hip, l3_greedy_step_host)
-__global__ void kv_restore_kernel(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos) {
+// Put back one cache slot from kv_bak (the run-ahead undo).  With a guard (the persistent batch-1
+// step, B = 1), what to put back is decided on the device when the restore runs, stream-ordered
+// after the steps it undoes: nothing if no step gave up; else nothing past the failed position,
+// everything before it, and at it only the units whose layer workgroup stored its write mark under
+// the failing launch's tag (decode_persist.hip: it wrote those slots and their kv_bak entries)
+__global__ void kv_restore_kernel(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos,
+                                  KvGuard g) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B * KVH * HD) return;
     const int d = i % HD, bh = i / HD;  // bh = b * KVH + h
+    if (g.err) {
+        const unsigned e = __hip_atomic_load(g.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (e) {
+            const int fp = (int)e - 1;
+            if (pos > fp) return;  // never ran
+            if (pos == fp) {       // ran up to its give-up: the units its workgroups wrote
+                const int wg = ((g.col_base + i) >> 1) / g.per;
+                if (g.wmarks[wg] != g.epoch[2]) return;
+            }
+        }
+    }
     if (i == 0) L3_DCHECK(pos >= 0 && pos < Smax, CHK_KV_SLOT);
     cache[((int64_t)bh * Smax + pos) * HD + d] = bak[i];
 }
 
 hipError_t launch_kv_restore(float* cache, const float* bak, int B, int KVH, int Smax, int HD, int pos,
-                             hipStream_t s) {
+                             hipStream_t s, KvGuard g) {
     const int n = B * KVH * HD;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(kv_restore_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, cache, bak, B, KVH,
-                       Smax, HD, pos);
+                       Smax, HD, pos, g);
     return hipGetLastError();
 }
 

@@ -221,6 +221,10 @@ struct l3_ctx {
     // graph-only for the rest of the context's life: a persistent step gave up on a hand-off
     // (persist_recover) or its launch was refused inside a capture (capture_steps)
     bool persist_off = false;
+    // spec_resolve queued a guarded undo behind persistent steps without waiting for them: a
+    // give-up among them is noticed (and the context turned graph-only) by persist_settle, at the
+    // next decode entry point, before any further persistent step is launched
+    bool persist_unsettled = false;
     int64_t persist_recoveries = 0;  // steps recovered on the graph path (stats)
     hipEvent_t order_ev = nullptr;   // after this context's last decode graph (launch_decode_graph)
 };
@@ -1046,8 +1050,9 @@ static int persist_setup(l3_ctx* c) {
     const int64_t slab = decode_persist_slab(a.H, a.KVH, a.HD, a.D, a.FD);
     const size_t ptr_bytes = (size_t)6 * nl * sizeof(void*);
     const size_t gran_off = (ptr_bytes + 16 + 255) & ~(size_t)255;
-    // per-layer slabs, the lm_head partials [2 x 256], the start marks [256]
-    const size_t gran_bytes = (size_t)(slab * nl + 3 * 256) * 8;
+    // per-layer slabs, the lm_head partials [2 x 256], the start marks [256], the write marks
+    // [GL] (32-bit, in a 256-granule block)
+    const size_t gran_bytes = (size_t)(slab * nl + 4 * 256) * 8;
     HIP_TRY(hipMalloc(&c->persist_mem, gran_off + gran_bytes));
     HIP_TRY(hipMemset(c->persist_mem, 0, gran_off + gran_bytes));
     std::vector<const void*> ptrs((size_t)6 * nl);
@@ -1105,34 +1110,57 @@ static void spec_drop_queue(l3_ctx* c) {
     c->spec_base = c->spec_end = 0;
 }
 
+// The undo's guard for one cache (sec 1: K, 2: V) of the persistent step (kv_restore_kernel)
+static KvGuard persist_guard(const l3_ctx* c, int sec) {
+    KvGuard g{};
+    if (!c->persist_ready || c->spec_B != 1) return g;
+    const DecodePersistArgs& a = c->persist;
+    const int qdim = a.H * a.HD, kvdim = a.KVH * a.HD, qkvn = qdim + 2 * kvdim;
+    g.err = c->persist_err_dev;
+    g.epoch = a.epoch;
+    g.wmarks = reinterpret_cast<const unsigned*>(a.gran + decode_persist_slab(a.H, a.KVH, a.HD, a.D, a.FD) * a.n_layers +
+                                                 3 * 256);
+    g.col_base = qdim + (sec - 1) * kvdim;
+    g.per = (qkvn / 2 + a.GL - 1) / a.GL;
+    return g;
+}
+
+// Queue the undo of every run-ahead step nobody has taken (stream-ordered after them): each
+// step's K / V slot in every layer back from kv_bak.  Guarded on the device when persistent steps
+// may be among them (a step that gave up: nothing from it on, and of it only what its workgroups
+// wrote; KvGuard), so the host need not wait for the queue to drain first.
+static int spec_undo(l3_ctx* c) {
+    const int KVH = c->d.n_kv_heads, HD = c->HD, n = c->spec_B * KVH * HD;
+    const bool guard = c->persist_ready && !c->persist_off;
+    const KvGuard gk = guard ? persist_guard(c, 1) : KvGuard{}, gv = guard ? persist_guard(c, 2) : KvGuard{};
+    for (int pos = c->spec_base; pos < c->spec_end; ++pos) {
+        for (size_t li = 0; li < c->layers.size(); ++li) {
+            const float* bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * KVH * HD + (int64_t)(pos % KV_BAK_SLOTS) * 2 * n;
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_k, bak, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream, gk));
+            HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream, gv));
+        }
+    }
+    spec_drop_queue(c);
+    return 0;
+}
+
 // Recovery from a persistent step that gave up (decode_persist.hip: its position + 1 in the error
-// word; every launch queued after it returned at once, the sticky word set).  With the stream
-// drained: the run-ahead steps nobody has taken are undone — those before the failed one in full
-// from kv_bak, the failed one only if it reached its cache write (epoch[2]; else it wrote no cache
-// slot), none after it (they never ran) — the failure words are cleared, and the context turns
-// graph-only: its decode graphs are dropped, so the caller's step runs eagerly and the next
+// word, its tag in epoch[2]; every launch queued after it returned at once, the sticky word set).
+// With the stream drained: the run-ahead steps nobody has taken are undone (spec_undo: on the
+// device, the failed step only where it wrote), the failure words are cleared, and the context
+// turns graph-only: its decode graphs are dropped, so the caller's step runs eagerly and the next
 // capture is the 25-kernel graph.  *failed_pos: the step to run again.
 static int persist_recover(l3_ctx* c, int* failed_pos) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int fp = (int)*c->persist_err - 1;
     unsigned w[3] = {0, 0, 0};
     HIP_TRY(hipMemcpy(w, c->persist.epoch, sizeof w, hipMemcpyDeviceToHost));
-    const bool wrote = w[2] == (unsigned)fp + 1u;
-    const int KVH = c->d.n_kv_heads, HD = c->HD;
-    for (int pos = c->spec_base; pos < c->spec_end; ++pos) {
-        if (pos > fp || (pos == fp && !wrote)) continue;
-        const int n = c->spec_B * KVH * HD;
-        for (size_t li = 0; li < c->layers.size(); ++li) {
-            const float* bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * KVH * HD + (int64_t)(pos % KV_BAK_SLOTS) * 2 * n;
-            HIP_TRY(launch_kv_restore(c->layers[li].cache_k, bak, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
-            HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
-        }
-    }
-    spec_drop_queue(c);
-    const unsigned fresh[3] = {w[0] + 1u, 0u, 0u};  // a tag no granule carries; sticky and cache words cleared
+    if (spec_undo(c)) return 1;  // reads the error word: cleared only after these ran
+    const unsigned fresh[3] = {w[0] + 1u, 0u, 0u};  // a tag no granule carries; sticky and failed-tag words cleared
     HIP_TRY(hipMemcpyAsync(c->persist.epoch, fresh, sizeof fresh, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     *c->persist_err = 0;
+    c->persist_unsettled = false;
     c->persist_off = true;
     drop_decode_graph(c);
     c->persist_graph = false;
@@ -1140,6 +1168,16 @@ static int persist_recover(l3_ctx* c, int* failed_pos) {
     c->persist_recoveries++;
     if (failed_pos) *failed_pos = fp;
     return 0;
+}
+
+// A guarded undo was queued without waiting (spec_resolve): before anything launches another
+// persistent step, see whether a step it undid had given up, and if so finish the recovery (the
+// undo itself has run: nothing is left in the queue)
+static int persist_settle(l3_ctx* c) {
+    if (!c->persist_unsettled) return 0;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->persist_unsettled = false;
+    return persist_failed(c) ? persist_recover(c, nullptr) : 0;
 }
 
 // Capture `steps` consecutive decode steps (B sequences, L = 1), each reading its position from
@@ -1170,6 +1208,7 @@ static int capture_steps(l3_ctx* c, int B, int steps, hipGraph_t* graph, hipGrap
             const bool inject_ok = env_knob("L3_TEST_FAULT_INJECTION", 0) == 1;
             a.fault_pos = inject_ok ? env_knob("L3_DECODE_PERSIST_FAULT", -1) : -1;
             a.fault_wg = env_knob("L3_DECODE_PERSIST_FAULT_WG", 1);
+            a.fault_late = env_knob("L3_DECODE_PERSIST_FAULT_LATE", 0);
             refused = launch_decode_persist(a, pgrid, c->stream) != hipSuccess;
         }
         // batch 1 (graph path): each step's argmax folded into the next step's layer-0 QKV, one
@@ -1372,21 +1411,12 @@ static int spec_resolve(l3_ctx* c) {
     if (c->spec_q.empty()) return 0;
     HIP_TRY(hipSetDevice(c->device));
     c->gather_tail = false;  // the restores below are queued after the gather
-    // persistent steps queued: one that gave up leaves its own slot and every later one unwritten,
-    // so the undo waits for them and takes the failure into account (persist_recover)
-    if (c->persist_ready && !c->persist_off) {
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (persist_failed(c)) return persist_recover(c, nullptr);
-    }
-    const int KVH = c->d.n_kv_heads, HD = c->HD, n = c->spec_B * KVH * HD;
-    for (int pos = c->spec_base; pos < c->spec_end; ++pos) {
-        for (size_t li = 0; li < c->layers.size(); ++li) {
-            const float* bak = c->kv_bak + (int64_t)li * KV_BAK_SLOTS * 2 * 8 * KVH * HD + (int64_t)(pos % KV_BAK_SLOTS) * 2 * n;
-            HIP_TRY(launch_kv_restore(c->layers[li].cache_k, bak, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
-            HIP_TRY(launch_kv_restore(c->layers[li].cache_v, bak + n, c->spec_B, KVH, c->d.max_seq_len, HD, pos, c->stream));
-        }
-    }
-    spec_drop_queue(c);
+    // persistent steps queued: one that gives up leaves its own slot partly or not at all written
+    // and every later one unwritten; the guarded undo decides that on the device, after them, so
+    // the caller does not wait here for the run-ahead to drain (persist_settle checks later)
+    const bool persist = c->persist_ready && !c->persist_off;
+    if (spec_undo(c)) return 1;
+    if (persist) c->persist_unsettled = true;
     c->dec_pos_mirror = -1;
     return 0;
 }
@@ -1394,7 +1424,8 @@ static int spec_resolve(l3_ctx* c) {
 extern "C" int l3_greedy_step_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
                                    int32_t start_pos, int64_t* next_ids_host, float* logits_host) {
     CHECK_CTX(c);
-    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L)) return 1;
+    if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c) || ensure_ws(c, B, L) || persist_settle(c))
+        return 1;
     if (!c->dec_ids) {
         HIP_TRY(hipMalloc(&c->dec_ids, (size_t)c->d.max_batch_size * 4));
         HIP_TRY(hipMalloc(&c->dec_state, sizeof(DecState)));

@@ -94,14 +94,17 @@ def test_persistent_decode_needs_its_cus(tmpdir_mod, monkeypatch):
     assert m2.context.decode_persistent()
 
 
-# (fault position, workgroup that gives up): a layer workgroup at the step's start — no stage
-# completes, the step writes no cache slot — or an lm workgroup — the layers complete and the
-# step writes its K / V slots before the launch fails (epoch[2]), so an undo must restore them
-FAULTS = [(30, 1), (41, 255)]
+# (fault position, workgroup that gives up, late): a layer workgroup at the step's start — no
+# stage completes, the step writes no cache slot — or an lm workgroup — the layers complete and
+# the step writes its K / V slots before the launch fails, so an undo must restore them — or
+# (late) a layer workgroup at its last wait of the step: every other layer workgroup writes its
+# slots and this one does not, so an undo must restore exactly the others' units (their write
+# marks carry the failing launch's tag, decode_persist.hip / kv_restore_kernel)
+FAULTS = [(30, 1, 0), (41, 255, 0), (33, 30, 1), (38, 50, 1)]  # wg 30: K units, wg 50: V units
 
 
-@pytest.mark.parametrize("fault_pos,fault_wg", FAULTS)
-def test_persistent_decode_fault_recovers_device_loop(tmpdir_mod, monkeypatch, fault_pos, fault_wg):
+@pytest.mark.parametrize("fault_pos,fault_wg,late", FAULTS)
+def test_persistent_decode_fault_recovers_device_loop(tmpdir_mod, monkeypatch, fault_pos, fault_wg, late):
     """One workgroup gives up in the step at fault_pos (L3_DECODE_PERSIST_FAULT, inside an 8-step
     graph of the device loop): every later launch of the graph returns at once; the loop
     recovers — clears the failure words, turns the context graph-only — and runs the rest from
@@ -113,6 +116,7 @@ def test_persistent_decode_fault_recovers_device_loop(tmpdir_mod, monkeypatch, f
     monkeypatch.setenv("L3_TEST_FAULT_INJECTION", "1")
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", str(fault_pos))
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_LATE", str(late))
     m = llama3.Llama(path, args)
     ids, vals = m.context.greedy_generate(prompt, n, values=True)
     np.testing.assert_array_equal(ids, want)
@@ -125,8 +129,8 @@ def test_persistent_decode_fault_recovers_device_loop(tmpdir_mod, monkeypatch, f
     np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
 
 
-@pytest.mark.parametrize("fault_pos,fault_wg", FAULTS)
-def test_persistent_decode_fault_recovers_lazy(tmpdir_mod, monkeypatch, fault_pos, fault_wg):
+@pytest.mark.parametrize("fault_pos,fault_wg,late", FAULTS)
+def test_persistent_decode_fault_recovers_lazy(tmpdir_mod, monkeypatch, fault_pos, fault_wg, late):
     """The same fault under the lazy generator with run-ahead (llama3.py:310-321: one step per
     yield, the device up to 16 steps ahead): the step that finds the failure undoes every
     queued step — those before the failed one in full, the failed one if it wrote its slots,
@@ -139,6 +143,7 @@ def test_persistent_decode_fault_recovers_lazy(tmpdir_mod, monkeypatch, fault_po
     monkeypatch.setenv("L3_TEST_FAULT_INJECTION", "1")
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", str(fault_pos))
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_LATE", str(late))
     m = llama3.Llama(path, args)
     got = np.concatenate(list(m.generate(prompt, n)), axis=1)
     np.testing.assert_array_equal(got, want)
@@ -151,17 +156,21 @@ def test_persistent_decode_fault_recovers_lazy(tmpdir_mod, monkeypatch, fault_po
     np.testing.assert_array_equal(np.concatenate(list(m.generate(prompt, n)), axis=1), want)
 
 
-def test_persistent_decode_fault_in_abandoned_run_ahead(tmpdir_mod, monkeypatch):
+@pytest.mark.parametrize("fault_wg,late", [(255, 0), (30, 1)])
+def test_persistent_decode_fault_in_abandoned_run_ahead(tmpdir_mod, monkeypatch, fault_wg, late):
     """The fault lands in a step the device ran ahead: the consumer stops before it (an
-    abandoned generator).  Whichever call finds the failure — a served step's chunk sync, or the
-    next call's undo of the abandoned run-ahead (spec_resolve) — restores only the slots the
-    steps that ran wrote, and the following full generation is exact."""
+    abandoned generator).  The next call's undo of the abandoned run-ahead (spec_resolve) is
+    queued without waiting and decides on the device what to restore (KvGuard): only the slots
+    the steps that ran wrote — for the failed step, only its workgroups that wrote (late: all
+    but workgroup 30) — and the next decode entry point finishes the recovery (persist_settle);
+    the following full generation is exact."""
     g, args, path = _stories(tmpdir_mod, "sharp")
     prompt, want, n = _dream(g)
     monkeypatch.setenv("L3_DECODE_PERSIST", "1")
     monkeypatch.setenv("L3_TEST_FAULT_INJECTION", "1")
     monkeypatch.setenv("L3_DECODE_PERSIST_FAULT", "20")
-    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", "255")
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_WG", str(fault_wg))
+    monkeypatch.setenv("L3_DECODE_PERSIST_FAULT_LATE", str(late))
     m = llama3.Llama(path, args)
     gen = m.generate(prompt, n)
     first = [next(gen) for _ in range(10)]  # positions 5..14 handed out; 15.. queued ahead
