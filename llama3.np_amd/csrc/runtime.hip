@@ -94,6 +94,7 @@ struct l3_ctx {
     static constexpr int MAX_PARTS = 4;
     hipStream_t aux[MAX_PARTS - 1] = {};
     hipEvent_t fork_ev = nullptr, join_ev[MAX_PARTS - 1] = {};
+    hipEvent_t lag_ev = nullptr;  // host path: the later parts' last layers wait for part 0's (forward_dev)
     int split = 2;                   // parts (1 = off); l3_set_batch_split, L3_BATCH_SPLIT
     bool prune_last = true;          // last layer: attention / O-proj / FFN on the last rows only
                                      // (l3_set_last_layer_rows, L3_LAST_LAYER_ALL_ROWS)
@@ -225,6 +226,7 @@ struct l3_ctx {
     // give-up among them is noticed (and the context turned graph-only) by persist_settle, at the
     // next decode entry point, before any further persistent step is launched
     bool persist_unsettled = false;
+    int host_lag = 2;  // forward_dev: host-path lag of the later batch parts (layers; tools/host_path_probe.py)
     int64_t persist_recoveries = 0;  // steps recovered on the graph path (stats)
     hipEvent_t order_ev = nullptr;   // after this context's last decode graph (launch_decode_graph)
 };
@@ -419,7 +421,8 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     auto bail = [&](int rc) { l3_destroy(c); return rc; };
     if (set_dev(c)) return bail(1);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->lag_ev, hipEventDisableTiming) != hipSuccess)
         return bail(fail("hipStreamCreate / hipEventCreate failed"));
     for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i)
         if (hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking) != hipSuccess ||
@@ -503,6 +506,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
         if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    if (c->lag_ev) (void)hipEventDestroy(c->lag_ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -860,8 +864,11 @@ static int fold_parts(l3_ctx* c, int B) {
 // logits_host (optional): each part's rows are copied back on that part's own stream right
 // after its lm_head, so part 0's D2H overlaps part 1's last layer and the parts' copies run
 // concurrently (two DMA queues); the join below covers them
+// host_pitch / host_off (a group member's rows): local row r lands in host row host_off +
+// host_pitch * r (the group's interleave, one 2-D copy per part over this member's own link)
 static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
-                       float* logits_dev, const int* pos_dev = nullptr, float* logits_host = nullptr) {
+                       float* logits_dev, const int* pos_dev = nullptr, float* logits_host = nullptr,
+                       int host_pitch = 1, int host_off = 0) {
     // roctx ranges (host-side launch spans; `rocprofv3 --marker-trace`) per block and lm_head
     static const char* names[] = {"l3.layer0", "l3.layer1", "l3.layer2", "l3.layer3", "l3.layer4",
                                   "l3.layer5", "l3.layer6", "l3.layer7", "l3.layerN"};
@@ -900,11 +907,21 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
         lm_parts = gemm_store_config(lm_head_args(c, nb[p], L, logits_dev, b0[p])) == lm_cfg;
     int rc = 0;
     const int nl = (int)c->layers.size();
+    // host path (logits_host): the logits copy is PCIe-bound (32.8 MB at C3, ~0.59 ms at 56 GB/s)
+    // and can start only once a part's logits exist; in lockstep both parts reach their lm_heads
+    // together and the whole copy is exposed.  With lag k the later parts' last k layers each
+    // wait for part 0's same layer, so part 0 reaches its lm_head and starts its copy while the
+    // others still compute (L3_HOST_LAG; lockstep elsewhere: desynchronised parts pack worse)
+    const int host_lag_env = env_knob("L3_HOST_LAG", -1);
+    const int lag = logits_host && parts > 1 ? (host_lag_env >= 0 ? host_lag_env : c->host_lag) : 0;
     for (int li = 0; li < nl && !rc; ++li) {
         roctxRangePushA(names[li < 8 ? li : 8]);
-        for (int p = 0; p < parts && !rc; ++p)
+        for (int p = 0; p < parts && !rc; ++p) {
+            if (p > 0 && li >= nl - lag) HIP_TRY(hipStreamWaitEvent(st[p], c->lag_ev, 0));
             rc = run_layer(c, li, nb[p], L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr, b0[p], st[p],
                            c->prune_last && li == nl - 1 && li > 0);
+            if (!rc && p == 0 && li >= nl - lag) HIP_TRY(hipEventRecord(c->lag_ev, st[0]));
+        }
         roctxRangePop();
     }
     // the previous step's gather may still read the logits rows: the lm_head streams wait for
@@ -916,8 +933,15 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
     const int64_t VS = c->d.vocab_size;
     auto d2h_rows = [&](int r0, int n, hipStream_t s) -> int {
         if (!logits_host || !n) return 0;
-        HIP_TRY(hipMemcpyAsync(logits_host + (int64_t)r0 * VS, logits_dev + (int64_t)r0 * VS,
-                               (size_t)n * VS * 4, hipMemcpyDeviceToHost, s));
+        if (host_pitch == 1) {
+            HIP_TRY(hipMemcpyAsync(logits_host + ((int64_t)host_off + r0) * VS, logits_dev + (int64_t)r0 * VS,
+                                   (size_t)n * VS * 4, hipMemcpyDeviceToHost, s));
+        } else {
+            const size_t w = (size_t)VS * 4;
+            HIP_TRY(hipMemcpy2DAsync(logits_host + ((int64_t)host_off + (int64_t)host_pitch * r0) * VS,
+                                     w * host_pitch, logits_dev + (int64_t)r0 * VS, w, w, (size_t)n,
+                                     hipMemcpyDeviceToHost, s));
+        }
         return 0;
     };
     roctxRangePushA("l3.lm_head");
@@ -966,12 +990,21 @@ static int upload_ids(l3_ctx* c, const int64_t* ids_host, int64_t T) {
         c->ids_pin_n = T;
     }
     const int64_t VS = c->d.vocab_size;
+    // two branch-free passes (both vectorise): the range check, then the NumPy wrap of negatives
+    int64_t lo = 0, hi = 0;
     for (int64_t i = 0; i < T; ++i) {
-        int64_t v = ids_host[i];
-        if (v < -VS || v >= VS)  // NumPy fancy indexing raises IndexError here (llama3.py:287)
-            return fail("token id %lld out of range for vocab_size %lld", (long long)v, (long long)VS);
-        if (v < 0) v += VS;  // ...and wraps negatives
-        c->ids_pin[i] = (int32_t)v;
+        lo = ids_host[i] < lo ? ids_host[i] : lo;
+        hi = ids_host[i] > hi ? ids_host[i] : hi;
+    }
+    if (lo < -VS || hi >= VS) {  // NumPy fancy indexing raises IndexError here (llama3.py:287)
+        for (int64_t i = 0; i < T; ++i)
+            if (ids_host[i] < -VS || ids_host[i] >= VS)
+                return fail("token id %lld out of range for vocab_size %lld", (long long)ids_host[i], (long long)VS);
+    }
+    int32_t* const dst = c->ids_pin;
+    for (int64_t i = 0; i < T; ++i) {
+        const int64_t v = ids_host[i];
+        dst[i] = (int32_t)(v + (v < 0 ? VS : 0));  // ...and wraps negatives
     }
     HIP_TRY(hipMemcpyAsync(c->ids, c->ids_pin, T * 4, hipMemcpyHostToDevice, c->stream));
     return 0;
@@ -2254,8 +2287,6 @@ struct l3_group {
     l3_dims d{};                     // the model; max_batch_size the global batch
     float* gbuf = nullptr;           // member 0: the other members' logits rows, member order
     int64_t gbuf_rows = 0;
-    float* gout = nullptr;           // member 0: all rows in row order (host path)
-    int64_t gout_rows = 0;
     int32_t* gids = nullptr;         // member 0: the other members' greedy ids
     int64_t gids_n = 0;
     std::vector<int64_t> tmp;        // host: one member's ids rows
@@ -2279,7 +2310,7 @@ extern "C" int l3_group_destroy(l3_group* g) {
         if (c) { (void)hipSetDevice(c->device); (void)hipStreamSynchronize(c->stream); }
     if (!g->m.empty() && g->m[0]) {
         (void)hipSetDevice(g->m[0]->device);
-        dfree(g->gbuf); dfree(g->gout); dfree(g->gids);
+        dfree(g->gbuf); dfree(g->gids);
         for (hipEvent_t e : g->rows_ev) if (e) (void)hipEventDestroy(e);
         if (g->copied_ev) (void)hipEventDestroy(g->copied_ev);
     }
@@ -2382,8 +2413,10 @@ extern "C" int l3_group_synchronize(l3_group* g) {
 // every member with rows: checks (all before any launch), then ids (host rows r = i + n*j, or
 // the member's device block) and its forward into its own logits workspace, launched without
 // waiting; each member's decode state is left (no graph replays in a multi-member call)
+// logits_host: each member also copies its rows straight into the caller's array (row i + n*j),
+// over its own PCIe link, right after each of its parts' lm_head (forward_dev host_pitch)
 static int group_launch(l3_group* g, const int64_t* ids_host, const int32_t* const* ids_dev, int B, int L,
-                        int start_pos) {
+                        int start_pos, float* logits_host = nullptr) {
     if (B > g->d.max_batch_size) return fail("batch %d exceeds max_batch_size %d", B, g->d.max_batch_size);
     if (B <= 0 || L <= 0) return fail("empty input: B=%d L=%d", B, L);
     for (int i = 0; i < g->n; ++i) {
@@ -2406,7 +2439,7 @@ static int group_launch(l3_group* g, const int64_t* ids_host, const int32_t* con
                 memcpy(&g->tmp[(size_t)j * L], ids_host + ((int64_t)i + (int64_t)g->n * j) * L, (size_t)L * 8);
             if (upload_ids(c, g->tmp.data(), (int64_t)nb * L)) return 1;
         }
-        if (forward_dev(c, ids, nb, L, start_pos, c->logits)) return 1;
+        if (forward_dev(c, ids, nb, L, start_pos, c->logits, nullptr, logits_host, g->n, i)) return 1;
     }
     return 0;
 }
@@ -2503,16 +2536,11 @@ extern "C" int l3_group_forward_host(l3_group* g, const int64_t* ids_host, int32
     if (!g || !ids_host || !logits_host) return fail("l3_group_forward_host: null argument");
     // rows on member 0 only: its own single-device host path (pinned per-part copies)
     if (!g->multi || B == 1) return l3_forward_host(g->m[0], ids_host, B, L, start_pos, logits_host);
-    const int64_t VS = g->d.vocab_size;
-    if (group_buf(g, &g->gbuf, &g->gbuf_rows, B - group_rows(g, B, 0), VS) ||
-        group_buf(g, &g->gout, &g->gout_rows, B, VS))
-        return 1;
-    if (group_launch(g, ids_host, nullptr, B, L, start_pos)) return 1;
-    std::vector<float*> src((size_t)g->n);
-    for (int i = 0; i < g->n; ++i) src[(size_t)i] = g->m[(size_t)i]->logits;
-    if (group_gather(g, B, VS, src.data(), g->gbuf, g->gout, ncclFloat32)) return 1;
-    l3_ctx* c0 = g->m[0];
-    HIP_TRY(hipMemcpyAsync(logits_host, g->gout, (size_t)B * VS * 4, hipMemcpyDeviceToHost, c0->stream));
+    // no gather: every member copies its own rows into the caller's (page-locked, portable) array
+    // over its own link, each batch part right after its lm_head — at C4 on 8 GPUs 32.8 MB per
+    // link in parallel (~0.6 ms) instead of 262 MB through member 0's one link (~4.7 ms).  The
+    // RCCL gather stays for l3_group_forward_dev (device-resident logits, north_star's gather)
+    if (group_launch(g, ids_host, nullptr, B, L, start_pos, logits_host)) return 1;
     return l3_group_synchronize(g);
 }
 

@@ -78,3 +78,68 @@ def test_group_virtual_members_match_single_device(model_path, single, monkeypat
     # a batched greedy loop through the group (ids gathered each step) equals the single device's
     pb = rng.integers(0, args.vocab_size, (5, 6))
     np.testing.assert_array_equal(grp.generate_all(pb, 30), single.generate_all(pb, 30))
+
+
+@pytest.fixture(scope="module")
+def c4_model():
+    """BASELINE configs[3] (C4: stories15M B = 2048, L = 256), default-scale weights (the plain
+    1e-4 bar applies), and a single-device model holding all 2048 rows."""
+    with tempfile.TemporaryDirectory() as d:
+        args = synth.stories15m(2048)
+        w = synth.make_weights(args, synth.STORIES15M_HIDDEN, seed=7)
+        path = os.path.join(d, "c4.npz")
+        synth.save_npz(path, w)
+        yield args, path, w, llama3.Llama(path, args)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_group_virtual_c4_partition(c4_model, monkeypatch, n):
+    """C4's own partition through the group on one GPU (n = 8: 256 rows per member, the 8-GPU
+    node's exact split; n = 2 / 4: the strong-scaling splits of the same batch).  Every member's
+    rows bit-identical to those rows run alone on one device — through the host path (each
+    member's per-link 2-D copy into the caller's array, l3_group_forward_host) and through the
+    device-resident gather (l3_group_forward_dev, north_star's single gather) alike — 8 spread
+    rows against the live oracle within 1e-4, and the greedy step's ids equal
+    (llama3.py:163-211, 285-308, 320)."""
+    import llama3_oracle as orc
+
+    monkeypatch.setenv("L3_GROUP_VIRTUAL", "1")
+    args, path, w, single = c4_model
+    B, L = 2048, 256
+    grp = llama3.Llama(path, args, devices=[0] * n)
+    g = grp.group
+    VS = args.vocab_size
+    ids = np.random.default_rng(2048 + n).integers(0, args.vocab_size, (B, L))
+    got = np.array(grp(ids, 0))
+    assert got.shape == (B, 1, VS) and np.isfinite(got).all()
+    # the device-resident path: member i's ids block on its context, the gather into member 0
+    ids_dev = []
+    for i, m in enumerate(g.members):
+        blk = np.ascontiguousarray(ids[i::n].astype(np.int32))
+        p = m.alloc(blk.size * 4)
+        m.h2d(p, blk)
+        ids_dev.append(p)
+    out_dev = g.members[0].alloc(B * VS * 4)
+    g.forward_dev(ids_dev, B, L, 0, out_dev)
+    g.synchronize()
+    dev = np.empty((B, VS), np.float32)
+    g.members[0].d2h(dev, out_dev)
+    np.testing.assert_array_equal(dev, got[:, 0, :])
+    g.members[0].free(out_dev)
+    for m, p in zip(g.members, ids_dev):
+        m.free(p)
+    # greedy ids of a 3-token chunk at positions 250-252 over the caches just written
+    nxt_g, _ = g.greedy_step(ids[:, 250:253], 250)
+    rows = [0, 255, 256, 777, 1023, 1024, 1500, 2047]
+    ref = orc.OracleModel(w, synth.stories15m(len(rows)))
+    err = float(np.max(np.abs(got[rows, 0].astype(np.float64) - ref(ids[rows], 0)[:, 0])))
+    assert err <= 1e-4, f"n={n}: spread rows vs the oracle max-abs {err:.3e}"
+    del grp, g
+    # each member's rows alone on one device: the same logits bit for bit, the same next ids
+    for i in range(n):
+        np.testing.assert_array_equal(got[i::n], single(ids[i::n], 0), err_msg=f"member {i} of {n}")
+        nxt_s, _ = single.context.greedy_step(ids[i::n, 250:253], 250)
+        np.testing.assert_array_equal(nxt_g[i::n], nxt_s, err_msg=f"member {i} greedy ids")
+    print(f"C4 partition n={n}: members bit-identical (per-link host copies and the gather), "
+          f"oracle max-abs {err:.2e}")

@@ -63,6 +63,19 @@ def main():
     res = {"forward_dev_ms": round(timeit(dev, 10), 4), "host_path_ms": round(timeit(host, 10), 4),
            "d2h_32.8MB_ms": round(timeit(d2h, 10), 4), "h2d_ids_ms": round(timeit(h2d, 10), 4)}
     res["d2h_GBps"] = round(B * VS * 4 / res["d2h_32.8MB_ms"] / 1e6, 1)
+    # the later batch part's last k layers wait for part 0's (L3_HOST_LAG, runtime.hip
+    # forward_dev): part 0's logits copy starts while part 1 still computes; interleaved rounds
+    lags = [int(x) for x in os.environ.get("PROBE_LAGS", "0,1,2,3").split(",")]
+    for rnd in range(2):
+        for k in lags:
+            os.environ["L3_HOST_LAG"] = str(k)
+            res[f"host_path_lag{k}_ms_r{rnd}"] = round(timeit(host, 20), 4)
+    os.environ.pop("L3_HOST_LAG", None)
+    x = m(ids, 0)
+    for k in lags:  # every lag returns the same logits
+        os.environ["L3_HOST_LAG"] = str(k)
+        res[f"lag{k}_bitwise_equal"] = bool(np.array_equal(m(ids, 0), x))
+    os.environ.pop("L3_HOST_LAG", None)
     ctx.set_batch_split(1)
     res["forward_dev_split1_ms"] = round(timeit(dev, 10), 4)
     res["host_path_split1_ms"] = round(timeit(host, 10), 4)
