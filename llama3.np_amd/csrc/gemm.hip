@@ -165,12 +165,16 @@ static hipError_t launch_skinny(const GemmArgs& a, hipStream_t s) {
     // loop of tools/gemm_tune) CH 6 / 12 measured 0.333 / 0.408 ms per B = 256 step against 0.313
     // (profiles/r05_skinny_ab.txt); L3_SKINNY_CH re-runs that A/B
     static const int ch = env_knob("L3_SKINNY_CH", 2);
+    // tile order (GemmArgs::skinny_xcd, bit-identical either way): L3_SKINNY_XCD
+    static const bool xcd = env_knob("L3_SKINNY_XCD", 0) != 0;
+    GemmArgs g = a;
+    g.skinny_xcd = xcd;
     if (ch >= 12)
-        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 12>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 12>), dim3((unsigned)blocks), dim3(256), 0, s, g);
     else if (ch >= 6)
-        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 6>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 6>), dim3((unsigned)blocks), dim3(256), 0, s, g);
     else
-        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2>), dim3((unsigned)blocks), dim3(256), 0, s, g);
     return hipGetLastError();
 }
 
@@ -269,14 +273,19 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     static const int group_env = env_knob("L3_GEMM_GROUP_M", 8);
     GemmArgs ag = a;
     ag.group_m = a.K >= 1024 && !small_m ? group_env : 0;
+    // EPI_QKV: the division-free full-tile epilogue (gemm_kernel.h qkv_epilogue_full) where its
+    // shape conditions hold — heads in whole 16-column groups, every wave's 64 rows within two
+    // sequences; L3_QKV_FAST_EPI=0 keeps the generic epilogue (A/B; both round identically)
+    static const bool qkv_fast_env = env_knob("L3_QKV_FAST_EPI", 1) != 0;
+    ag.qkv_fast = epi == EPI_QKV && qkv_fast_env && a.HD % 16 == 0 && a.L >= 64;
     switch (epi) {
         case EPI_SWIGLU:  // 128 x 128, BK 16
             if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2, 32>(a, s);
             return launch<EPI_SWIGLU, 2, 2, 4, 4, 3, 16>(ag, s);
         case EPI_QKV:     // 128 x 96 at short K (stories15M), else 128 x 128; BK 16
-            if (small_m) return launch<EPI_QKV, 1, 4, 1, 2, 2, 32>(a, s);
-            if (a.N % 96 == 0 && a.K <= 1024) return launch<EPI_QKV, 2, 2, 4, 3, 4, 16>(a, s);
-            return launch<EPI_QKV, 2, 2, 4, 4, 3, 16>(a, s);
+            if (small_m) return launch<EPI_QKV, 1, 4, 1, 2, 2, 32>(ag, s);
+            if (a.N % 96 == 0 && a.K <= 1024) return launch<EPI_QKV, 2, 2, 4, 3, 4, 16>(ag, s);
+            return launch<EPI_QKV, 2, 2, 4, 4, 3, 16>(ag, s);
         case EPI_RESID:   // O-proj / down
             if (small_m) return launch<EPI_RESID, 1, 4, 1, 2, 2, 32>(a, s);
             if (a.N % 96 == 0)

@@ -161,6 +161,82 @@ __device__ __forceinline__ void qkv_epilogue(const GemmArgs& p, const f32x4 (&ac
     }
 }
 
+// The QKV epilogue of a tile that lies wholly inside the launch (block-uniform: the product C3 /
+// C4 / C5 shapes are multiples of their tiles) with HD % 16 == 0 and L >= the wave's TM x 16
+// rows: the same arithmetic as qkv_epilogue, without its per-element work — no bounds guards,
+// no integer division per row or column (each wave's first row and each 16-column group, which
+// a head never straddles, are split once on the scalar unit; a lane's rows add at most one
+// sequence wrap), each output address a row part plus a column part, and the q / k / v choice
+// per column group wave-uniform.  In-kernel stamps (tools/gemm_tune qkvstamps, round 6): the
+// generic epilogue took 21.5k cycles per block against 6.0k for a plain store of the same tile
+template <int TM, int TN, int TH = (TM > 1 ? TM / 2 : 1)>
+__device__ __forceinline__ void qkv_epilogue_full(const GemmArgs& p, const f32x4 (&acc)[TM][TN],
+                                                  const float (&rs)[TM], int mrow0, int ncol0, int lane) {
+    const int frow = lane & 15, fq4 = 4 * (lane >> 4);
+    const int qdim = p.H * p.HD, kvdim = p.KVH * p.HD, hd2 = p.HD >> 1;
+    const int sp = start_of(p);
+    const int L = p.L;
+    // rows: mrow0 (wave-uniform) = b0 * L + r0; lane row i: r0 + 16 i + frow < 2L
+    const int b0 = __builtin_amdgcn_readfirstlane(mrow0) / L;
+    const int r0 = __builtin_amdgcn_readfirstlane(mrow0) - b0 * L;
+    const int64_t bstride = (int64_t)p.KVH * p.Smax * p.HD;
+    int pos[TM];
+    int64_t qoff[TM], koff[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int local = r0 + i * 16 + frow;
+        const bool wrap = local >= L;
+        const int ps = wrap ? local - L : local;
+        pos[i] = sp + ps;
+        qoff[i] = (int64_t)(mrow0 + i * 16 + frow) * qdim;
+        koff[i] = (int64_t)(b0 + (wrap ? 1 : 0)) * bstride + (int64_t)pos[i] * p.HD;
+        L3_DCHECK(pos[i] >= 0 && pos[i] < p.Smax, CHK_KV_SLOT);
+    }
+    // column groups: section, head and the group's first d, all wave-uniform
+    int sec[TN];
+    int coff[TN], d[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int c0 = __builtin_amdgcn_readfirstlane(ncol0 + j * 16) + p.col_base;
+        const int sc = c0 < qdim ? 0 : (c0 < qdim + kvdim ? 1 : 2);
+        const int cc = c0 - (sc == 0 ? 0 : (sc == 1 ? qdim : qdim + kvdim));
+        const int head = cc / p.HD;
+        sec[j] = sc;
+        d[j] = cc - head * p.HD + fq4;
+        coff[j] = sc == 0 ? ncol0 + j * 16 + fq4 : head * p.Smax * p.HD + d[j];
+    }
+    // TH rows of tables per pass: every load of a pass is issued before its stores (a load's
+    // vmcnt wait also waits for older stores)
+#pragma unroll
+    for (int i0 = 0; i0 < TM; i0 += TH) {
+        float2 cs[TH][TN], sn[TH][TN];
+#pragma unroll
+        for (int ii = 0; ii < TH; ++ii)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int t = pos[i0 + ii] * hd2 + (d[j] >> 1);
+                cs[ii][j] = *reinterpret_cast<const float2*>(p.rope_cos + t);
+                sn[ii][j] = *reinterpret_cast<const float2*>(p.rope_sin + t);
+            }
+#pragma unroll
+        for (int ii = 0; ii < TH; ++ii) {
+            const int i = i0 + ii;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const bool rot = sec[j] < 2;
+                const float2 c = rot ? cs[ii][j] : float2{1.f, 1.f};
+                const float2 s = rot ? sn[ii][j] : float2{0.f, 0.f};
+                const f32x4 v = acc[i][j] * (sec[j] == 0 ? rs[i] * p.q_scale : rs[i]);
+                const f32x4 r = {v.x * c.x - v.y * s.x, v.x * s.x + v.y * c.x,
+                                 v.z * c.y - v.w * s.y, v.z * s.y + v.w * c.y};
+                float* base = sec[j] == 0 ? p.q_out : (sec[j] == 1 ? p.cache_k : p.cache_v);
+                const int64_t off = (sec[j] == 0 ? qoff[i] : koff[i]) + coff[j];
+                *reinterpret_cast<f32x4*>(base + off) = r;
+            }
+        }
+    }
+}
+
 // Register-direct epilogue (EPI_STORE / EPI_RESID / EPI_SWIGLU).  The MFMA operands are swapped
 // (W fragment as the A operand, activation fragment as B), so the accumulator of tile (i, j) is C^T: lane l
 // holds C[row = 16i + (l&15)][col = 16j + 4(l>>4) + r], r = 0..3 — four consecutive columns
@@ -622,7 +698,19 @@ __global__ void __launch_bounds__(64 * WM * WN, WAVES_PER_EU) gemm_lds_kernel(Ge
         rs[i] = p.norm ? __builtin_amdgcn_rsqf(v * inv_k + p.eps) : 1.0f;
     }
     L3_STAMP(2);
-    if constexpr (EPI == EPI_QKV) qkv_epilogue<TM, TN>(p, acc, rs, m0 + arow0, n0 + brow0, lane);
+    if constexpr (EPI == EPI_QKV) {
+        // whole tile inside the launch (block-uniform), heads in whole 16-column groups, at most
+        // one sequence wrap per wave row range: the division-free epilogue (L3_QKV_FAST_EPI=0
+        // in the launcher keeps the generic one for A/B)
+        if (p.qkv_fast && m0 + BM <= p.M && n0 + BN <= p.N)
+#ifdef L3_QKV_TH_ALL  // tools: every table load before the first store (register A/B)
+            qkv_epilogue_full<TM, TN, TM>(p, acc, rs, m0 + arow0, n0 + brow0, lane);
+#else
+            qkv_epilogue_full<TM, TN>(p, acc, rs, m0 + arow0, n0 + brow0, lane);
+#endif
+        else
+            qkv_epilogue<TM, TN>(p, acc, rs, m0 + arow0, n0 + brow0, lane);
+    }
     else direct_epilogue<TM, TN, EPI, RES_PREFETCH>(p, acc, rs, res, m0 + arow0, n0 + brow0, lane);
     L3_STAMP(3);
     if constexpr (STAMP) {
@@ -649,16 +737,37 @@ __global__ void __launch_bounds__(64 * WM * WN, WAVES_PER_EU) gemm_lds_kernel(Ge
 // four partial tiles (and row sums of squares) meet in LDS and wave 0 adds them in wave order
 // and runs the tiled kernel's epilogue (RMSNorm row factor, RoPE / KV append, SwiGLU pairs,
 // residual).  The weight-streaming GEMV keeps M <= 8, where its lanes' wider K split wins.
-template <int EPI, int TN, int CH, int NW = 4>
+//
+// STAMP (diagnostic builds, tools/gemm_tune skinnystamps; never in the product): wave 0 of each
+// block leaves s_memrealtime (100 MHz) stamps in p.stamps[block][8]: entry, first fragments
+// landed, k-loop done, partials reduced (after the barrier), epilogue issued, its stores acked
+template <int EPI, int TN, int CH, int NW = 4, bool STAMP = false>
 __global__ void __launch_bounds__(64 * NW) gemm_skinny_kernel(GemmArgs p) {
     static_assert(EPI != EPI_SWIGLU || TN % 2 == 0, "SwiGLU pairs gate / up tiles");
+    auto sk_stamp = [&](int k) {
+        if constexpr (STAMP) {
+            __builtin_amdgcn_sched_barrier(0);
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            if ((threadIdx.x & 255) == 0) p.stamps[(size_t)blockIdx.x * 8 + k] = t;
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    sk_stamp(0);
     constexpr int WN = 16 * TN;  // columns per tile
     __shared__ f32x4 red[NW][TN][64];
     __shared__ float rss[NW][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int frow = lane & 15, kq = 4 * (lane >> 4);
     const int ntn = (p.N + WN - 1) / WN;
-    const int mt = blockIdx.x / ntn, nt = blockIdx.x - mt * ntn;
+    int mt, nt;
+    if (p.skinny_xcd) {  // contiguous run of tiles per XCD, column-major: W tiles stay on one XCD
+        const int nmt = (p.M + 15) / 16, t = xcd_remap(blockIdx.x, gridDim.x);
+        nt = t / nmt;
+        mt = t - nt * nmt;
+    } else {
+        mt = blockIdx.x / ntn;
+        nt = blockIdx.x - mt * ntn;
+    }
     const int m0 = mt * 16, n0 = nt * WN;
     const float* arow = a_row(p, min(m0 + frow, p.M - 1));
     const float* wrow[TN];
@@ -694,6 +803,12 @@ __global__ void __launch_bounds__(64 * NW) gemm_skinny_kernel(GemmArgs p) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) wv[c][j] = *reinterpret_cast<const f32x4*>(wrow[j] + k);
         }
+        if constexpr (STAMP) {
+            if (kb0 == kb_lo) {
+                __builtin_amdgcn_s_waitcnt(0);  // (diagnostic) the first fragments landed
+                sk_stamp(1);
+            }
+        }
 #pragma unroll
         for (int c = 0; c < CH; ++c) {
             if (kb0 + c < kb_hi) {  // wave-uniform
@@ -705,11 +820,13 @@ __global__ void __launch_bounds__(64 * NW) gemm_skinny_kernel(GemmArgs p) {
             }
         }
     }
+    sk_stamp(2);
 #pragma unroll
     for (int j = 0; j < TN; ++j) red[wid][j][lane] = acc[0][j];
     rss[wid][lane] = ss;
     __syncthreads();
     if (wid != 0) return;
+    sk_stamp(3);
 #pragma unroll
     for (int w = 1; w < NW; ++w) {
 #pragma unroll
@@ -727,6 +844,11 @@ __global__ void __launch_bounds__(64 * NW) gemm_skinny_kernel(GemmArgs p) {
         direct_epilogue<1, TN, EPI, true, TN>(p, acc, rs, res, m0, n0, lane);
     } else {
         direct_epilogue<1, TN, EPI, false, 1>(p, acc, rs, res, m0, n0, lane);
+    }
+    if constexpr (STAMP) {
+        sk_stamp(4);
+        __builtin_amdgcn_s_waitcnt(0);  // (diagnostic) the epilogue's stores acknowledged
+        sk_stamp(5);
     }
 }
 

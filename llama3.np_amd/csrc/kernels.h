@@ -93,6 +93,12 @@ struct GemmArgs {
     int L, start_pos, H, KVH, HD, Smax;
     const int* pos_dev;            // if set, start_pos is read from device memory (graph replay)
     float q_scale;
+    // EPI_QKV on the tiled kernel: the division-free full-tile epilogue may run (set by the
+    // launcher when HD % 16 == 0 and L >= the tile's wave rows; gemm_kernel.h qkv_epilogue_full)
+    bool qkv_fast;
+    // gemm_skinny_kernel: tiles dealt to the XCDs in contiguous runs walked column-major, so one
+    // XCD's blocks share a few W column tiles in its L2 instead of every XCD pulling all of W
+    bool skinny_xcd;
     int col_base;                  // EPI_QKV on the tiled / skinny kernels: index of output column 0
                                    // in the [q | k | v] layout (W starts at that row of wqkv): a
                                    // pruned last block appends K / V for every row without q

@@ -75,6 +75,7 @@ static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
 // come from the MALL / HBM as in the batched decode loop (each XCD's 4 MB L2 evicted); per-launch
 // time = (flush + launch) - flush alone, both timed over the same iterations
 static bool g_cold = false;
+static bool g_qkv_fast = false;  // stamp_report: EPI_QKV with the division-free epilogue
 __global__ void flush_kernel(const f32x4* buf, int64_t n, float* sink) {
     f32x4 a = {0.f, 0.f, 0.f, 0.f};
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) a += buf[i];
@@ -139,12 +140,21 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
            (int)norm, flops / 1e9);
     // correctness vs variant 0 (RESID: start from zero output each time)
     std::vector<float> ref((size_t)M * outN), got((size_t)M * outN);
+    const size_t cache_n = epi == EPI_QKV ? (size_t)((M + 255) / 256) * 6 * 256 * 48 : 0;
+    std::vector<float> refk(cache_n), refv(cache_n), gotk(cache_n), gotv(cache_n);
     for (size_t v = 0; v < vars.size(); ++v) {
         CK(hipMemsetAsync(g.C, 0, (size_t)M * outN * 4, s));
+        if (cache_n) { CK(hipMemsetAsync(ck, 0, cache_n * 4, s)); CK(hipMemsetAsync(cv, 0, cache_n * 4, s)); }
         vars[v].run(g, s);
         CK(hipGetLastError());
         CK(hipStreamSynchronize(s));
         CK(hipMemcpy(v ? got.data() : ref.data(), g.C, got.size() * 4, hipMemcpyDeviceToHost));
+        if (cache_n) {  // EPI_QKV: the K / V cache slots too, bit for bit
+            CK(hipMemcpy(v ? gotk.data() : refk.data(), ck, cache_n * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(v ? gotv.data() : refv.data(), cv, cache_n * 4, hipMemcpyDeviceToHost));
+            if (v) printf("   check %-40s K cache %s, V cache %s\n", vars[v].name.c_str(),
+                          gotk == refk ? "bit-identical" : "DIFFERS", gotv == refv ? "bit-identical" : "DIFFERS");
+        }
         if (v) {
             double md = 0, mr = 0;
             for (size_t i = 0; i < got.size(); ++i) {
@@ -204,6 +214,17 @@ static void stamp_report(const char* label, int M, int K, int N, bool norm) {
     float *A, *W, *C;
     CK(hipMalloc(&A, (size_t)M * K * 4)); CK(hipMalloc(&W, (size_t)N * K * 4));
     CK(hipMalloc(&C, (size_t)M * outN * 4));
+    // EPI_QKV: the stories15M attention geometry (as run_shape), q / cache / RoPE tables
+    float *qo = nullptr, *ck = nullptr, *cv = nullptr, *rc = nullptr, *rsn = nullptr;
+    if (EPI == EPI_QKV) {
+        const size_t cache = (size_t)((M + 255) / 256) * 6 * 256 * 48;
+        CK(hipMalloc(&qo, (size_t)M * 288 * 4)); CK(hipMalloc(&ck, cache * 4)); CK(hipMalloc(&cv, cache * 4));
+        std::vector<float> tc(256 * 24), ts(256 * 24);
+        fill(tc, -1.f, 1.f, 4); fill(ts, -1.f, 1.f, 5);
+        CK(hipMalloc(&rc, tc.size() * 4)); CK(hipMalloc(&rsn, ts.size() * 4));
+        CK(hipMemcpy(rc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(rsn, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
+    }
     std::vector<float> hA((size_t)M * K), hW((size_t)N * K);
     fill(hA, -1.f, 1.f, 1); fill(hW, -0.05f, 0.05f, 2);
     CK(hipMemcpy(A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
@@ -215,6 +236,11 @@ static void stamp_report(const char* label, int M, int K, int N, bool norm) {
     GemmArgs g{};
     g.A = A; g.lda = K; g.W = W; g.C = C; g.ldc = outN; g.M = M; g.N = N; g.K = K;
     g.norm = norm; g.eps = 1e-6f; g.stamps = st;
+    if (EPI == EPI_QKV) {
+        g.H = 6; g.KVH = 6; g.HD = 48; g.L = 256; g.Smax = 256; g.start_pos = 0; g.q_scale = 0.2f;
+        g.q_out = qo; g.cache_k = ck; g.cache_v = cv; g.rope_cos = rc; g.rope_sin = rsn; g.C = qo; g.ldc = 288;
+        g.qkv_fast = g_qkv_fast;
+    }
     for (int it = 0; it < 20; ++it)  // back-to-back launches so the clock settles; last one kept
         hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, true, BK>), dim3(tiles), dim3(256), 0, 0, g);
     CK(hipDeviceSynchronize());
@@ -240,10 +266,151 @@ static void stamp_report(const char* label, int M, int K, int N, bool norm) {
            "launch span %.1f us, residency %.2f blocks/CU\n",
            label, WPE, BK, tiles, med(ratio), med(pro), med(loop), mfma_cycles, med(epi), span / 100.0,
            life / (span * 256.0));
+    // MFMA share of a CU's cycles: blocks x 4 waves x MFMA cycles / (4 SIMDs x 256 CUs x span
+    // in shader cycles), the span converted at the blocks' median clock
+    const double clk = med(ratio) * 1e6;  // Hz (s_memtime counts per 100 MHz realtime tick x 1e6)
+    const double occ = (double)tiles * 4.0 * mfma_cycles / (1024.0 * span / 1e8 * clk);
+    printf("   MFMA occupancy over the launch %.3f; at this clock the peak is %.1f TF/s (%.1f%% of 157.3)\n",
+           occ, 157.3 * clk / 2.4e9, 100.0 * clk / 2.4e9);
     CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(C)); CK(hipFree(st));
+    if (qo) { CK(hipFree(qo)); CK(hipFree(ck)); CK(hipFree(cv)); CK(hipFree(rc)); CK(hipFree(rsn)); }
+}
+
+// Round 6 (verdict r05 item 4): where a batched-decode skinny launch's time goes.  A decode-like
+// chain at M = B rows — per layer the QKV, O-proj, gate|up and down skinny GEMMs (TN and tiles of
+// the product at B = 256, own weights per layer: 6 layers, 24 MB), back to back on one stream,
+// STAMP build — and per launch: the gap from the previous launch's last block exit to this
+// launch's first block entry, the span from first entry to last exit, and per block (medians)
+// the first fragments' round trip, the rest of the k-loop, the wait at the partials' barrier,
+// the epilogue and its stores' acknowledgement.  All in 10 ns ticks of s_memrealtime.
+static int g_sk_ch = 2;
+template <int EPI, int TN>
+static void skinny_stamp_launch(GemmArgs g, hipStream_t s) {
+    const int blocks = ((g.M + 15) / 16) * ((g.N + 16 * TN - 1) / (16 * TN));
+    if (g_sk_ch >= 6) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 6, 4, true>), dim3(blocks), dim3(256), 0, s, g);
+    else if (g_sk_ch >= 3) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 3, 4, true>), dim3(blocks), dim3(256), 0, s, g);
+    else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2, 4, true>), dim3(blocks), dim3(256), 0, s, g);
+}
+static bool g_sk_xcd = false;
+static void skinny_stamps(int M, int reps) {
+    const int D = 288, FD = 768, NL = 6;
+    struct Sh { const char* name; int epi, K, N, TN; };
+    const Sh sh[4] = {{"QKV", EPI_QKV, D, 864, 1}, {"O-proj", EPI_RESID, D, D, 1},
+                      {"gate|up", EPI_SWIGLU, D, 2 * FD, 2}, {"down", EPI_RESID, FD, D, 1}};
+    std::vector<float*> W(4 * NL);
+    for (int l = 0; l < NL; ++l)
+        for (int k = 0; k < 4; ++k) {
+            std::vector<float> h((size_t)sh[k].N * sh[k].K);
+            fill(h, -0.05f, 0.05f, 10 + 4 * l + k);
+            CK(hipMalloc(&W[4 * l + k], h.size() * 4));
+            CK(hipMemcpy(W[4 * l + k], h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        }
+    float *x, *q, *hid, *ck, *cv, *rc, *rsn;
+    std::vector<float> hx((size_t)M * D);
+    fill(hx, -1.f, 1.f, 1);
+    CK(hipMalloc(&x, hx.size() * 4)); CK(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMalloc(&q, (size_t)M * D * 4)); CK(hipMalloc(&hid, (size_t)M * FD * 4));
+    CK(hipMalloc(&ck, (size_t)M * 6 * 256 * 48 * 4)); CK(hipMalloc(&cv, (size_t)M * 6 * 256 * 48 * 4));
+    std::vector<float> tc(256 * 24), ts(256 * 24);
+    fill(tc, -1.f, 1.f, 4); fill(ts, -1.f, 1.f, 5);
+    CK(hipMalloc(&rc, tc.size() * 4)); CK(hipMalloc(&rsn, ts.size() * 4));
+    CK(hipMemcpy(rc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(rsn, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
+    const int nl = 4 * NL;
+    int blk[4];
+    for (int k = 0; k < 4; ++k) blk[k] = ((M + 15) / 16) * ((sh[k].N + 16 * sh[k].TN - 1) / (16 * sh[k].TN));
+    std::vector<unsigned long long*> st(nl);
+    for (int i = 0; i < nl; ++i) {
+        CK(hipMalloc(&st[i], (size_t)blk[i % 4] * 8 * 8));
+        CK(hipMemset(st[i], 0, (size_t)blk[i % 4] * 8 * 8));
+    }
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    auto chain = [&]() {
+        for (int l = 0; l < NL; ++l)
+            for (int k = 0; k < 4; ++k) {
+                GemmArgs g{};
+                g.M = M; g.K = sh[k].K; g.N = sh[k].N; g.W = W[4 * l + k]; g.eps = 1e-6f; g.stamps = st[4 * l + k];
+                g.skinny_xcd = g_sk_xcd;
+                if (k == 0) {  // QKV, decode geometry: one row per sequence at position 100
+                    g.A = x; g.lda = D; g.norm = true; g.H = 6; g.KVH = 6; g.HD = 48; g.L = 1; g.Smax = 256;
+                    g.start_pos = 100; g.q_scale = 0.2f; g.q_out = q; g.cache_k = ck; g.cache_v = cv;
+                    g.rope_cos = rc; g.rope_sin = rsn;
+                    skinny_stamp_launch<EPI_QKV, 1>(g, s);
+                } else if (k == 1) {  // O-proj on q as the attention output, residual in place on x
+                    g.A = q; g.lda = D; g.C = x; g.ldc = D;
+                    skinny_stamp_launch<EPI_RESID, 1>(g, s);
+                } else if (k == 2) {
+                    g.A = x; g.lda = D; g.norm = true; g.C = hid; g.ldc = FD;
+                    skinny_stamp_launch<EPI_SWIGLU, 2>(g, s);
+                } else {
+                    g.A = hid; g.lda = FD; g.C = x; g.ldc = D;
+                    skinny_stamp_launch<EPI_RESID, 1>(g, s);
+                }
+            }
+    };
+    for (int r = 0; r < reps; ++r) chain();  // back to back; the last chain's stamps are read
+    CK(hipStreamSynchronize(s));
+    auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v.empty() ? 0.0 : v[v.size() / 2]; };
+    std::vector<std::vector<double>> gap(4), span(4), first(4), loop(4), red(4), epi(4), ack(4), life(4);
+    unsigned long long prev_exit = 0;
+    for (int i = 0; i < nl; ++i) {
+        std::vector<unsigned long long> h((size_t)blk[i % 4] * 8);
+        CK(hipMemcpy(h.data(), st[i], h.size() * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int b = 0; b < blk[i % 4]; ++b) {
+            const unsigned long long* d = &h[(size_t)b * 8];
+            t0 = std::min(t0, d[0]); t1 = std::max(t1, d[5]);
+            first[i % 4].push_back((double)(d[1] - d[0]));
+            loop[i % 4].push_back((double)(d[2] - d[1]));
+            red[i % 4].push_back((double)(d[3] - d[2]));
+            epi[i % 4].push_back((double)(d[4] - d[3]));
+            ack[i % 4].push_back((double)(d[5] - d[4]));
+            life[i % 4].push_back((double)(d[5] - d[0]));
+        }
+        if (prev_exit) gap[i % 4].push_back((double)t0 - (double)prev_exit);
+        span[i % 4].push_back((double)(t1 - t0));
+        prev_exit = t1;
+    }
+    double tot = 0;
+    for (int k = 0; k < 4; ++k) tot += (med(gap[k]) + med(span[k])) / 100;
+    printf("\n== skinny stamps M=%d CH=%d xcd-runs=%d: one layer's four launches %.2f us (us; medians over 6 layers' launches / their blocks; 10 ns ticks)\n",
+           M, g_sk_ch, (int)g_sk_xcd, tot);
+    for (int k = 0; k < 4; ++k)
+        printf("   %-8s blocks %4d  gap from previous launch %.2f  span %.2f | per block: life %.2f = first fragments %.2f "
+               "+ rest of k-loop %.2f + partials barrier %.2f + epilogue %.2f + stores acked %.2f\n",
+               sh[k].name, blk[k], med(gap[k]) / 100, med(span[k]) / 100, med(life[k]) / 100, med(first[k]) / 100,
+               med(loop[k]) / 100, med(red[k]) / 100, med(epi[k]) / 100, med(ack[k]) / 100);
 }
 
 int main(int argc, char** argv) {
+    if (argc > 3 && std::string(argv[3]) == "skinnystamps") {
+        for (int r = 0; r < 2; ++r)
+            for (int ch : {2, 3, 6})
+                for (int x : {0, 1}) {
+                    g_sk_ch = ch;
+                    g_sk_xcd = x;
+                    skinny_stamps(256, 20);
+                }
+        g_sk_ch = 2;
+        g_sk_xcd = false;
+        skinny_stamps(64, 20);
+        g_sk_xcd = true;
+        skinny_stamps(64, 20);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "qkvstamps") {  // round 6: the real QKV epilogue
+        for (int r = 0; r < 2; ++r) {
+            stamp_report<2, 2, 4, 3, EPI_QKV, 4, 16>("QKV 128x96 (+RoPE, KV append)", 65536, 288, 864, true);
+            g_qkv_fast = true;
+            stamp_report<2, 2, 4, 3, EPI_QKV, 4, 16>("QKV 128x96 fast epilogue", 65536, 288, 864, true);
+            g_qkv_fast = false;
+            stamp_report<2, 2, 4, 3, EPI_STORE, 4, 16>("QKV-shape 128x96 plain store", 65536, 288, 864, true);
+            stamp_report<2, 2, 4, 4, EPI_QKV, 3, 16>("QKV 128x128 (+RoPE, KV append)", 65536, 288, 864, true);
+            stamp_report<2, 2, 4, 4, EPI_SWIGLU, 3, 16>("gate|up 128x128", 65536, 288, 1536, true);
+        }
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "stamps") {
         stamp_report<2, 2, 4, 4, EPI_SWIGLU, 3, 16>("gate|up 128x128", 65536, 288, 1536, true);
         stamp_report<2, 2, 4, 3, EPI_STORE, 4, 16>("QKV-shape 128x96", 65536, 288, 864, true);
@@ -428,6 +595,49 @@ int main(int argc, char** argv) {
                        GVARN(2, 2, 4, 2, EPI_STORE, 3, 16, 3), GVARN(1, 4, 4, 2, EPI_STORE, 2, 16, 4),
                        GVARN(2, 2, 1, 4, EPI_STORE, 2, 16, 6)},
                       rounds, iters);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "qkvfast") {  // round 6: the division-free QKV epilogue
+        Variant fast{"glds<2,2,4,3,wpe4,bk16> fast epilogue", [](const GemmArgs& a0, hipStream_t s) {
+            GemmArgs a = a0;
+            a.qkv_fast = true;
+            hipLaunchKernelGGL((gemm_lds_kernel<2, 2, 4, 3, EPI_QKV, 4, false, 16, true>), dim3(512 * 9), dim3(256), 0, s, a);
+        }};
+        Variant fast128{"glds<2,2,4,4,wpe3,bk16> fast epilogue", [](const GemmArgs& a0, hipStream_t s) {
+            GemmArgs a = a0;
+            a.qkv_fast = true;
+            hipLaunchKernelGGL((gemm_lds_kernel<2, 2, 4, 4, EPI_QKV, 3, false, 16, true>), dim3(512 * 7), dim3(256), 0, s, a);
+        }};
+        for (int r = 0; r < 2; ++r) {
+            run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                      {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), fast, fast128}, rounds, iters);
+            run_shape("QKV shape, plain store", EPI_STORE, M, 288, 864, true,
+                      {GVAR(2, 2, 4, 3, EPI_STORE, 4, 16)}, rounds, iters);
+        }
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "qkvsplit") {  // round 6: QKV columns by two tiles
+        // columns [0, 768) on the 128 x 128 tile (16 MFMAs per 4-deep k-step, the gate|up tile:
+        // 6 column tiles, no padding) and [768, 864) on 128 x 96, as two launches
+        Variant two{"two launches 128x128 [0,768) + 128x96 [768,864)", [](const GemmArgs& a0, hipStream_t s) {
+            GemmArgs a = a0;
+            a.N = 768;
+            hipLaunchKernelGGL((gemm_lds_kernel<2, 2, 4, 4, EPI_QKV, 3, false, 16, true>), dim3(512 * 6), dim3(256), 0, s, a);
+            GemmArgs b = a0;
+            b.W = a0.W + (int64_t)768 * a0.K; b.N = 96; b.col_base = 768;
+            hipLaunchKernelGGL((gemm_lds_kernel<2, 2, 4, 3, EPI_QKV, 4, false, 16, true>), dim3(512), dim3(256), 0, s, b);
+        }};
+        Variant two4{"two launches 128x128 wpe4 + 128x96", [](const GemmArgs& a0, hipStream_t s) {
+            GemmArgs a = a0;
+            a.N = 768;
+            hipLaunchKernelGGL((gemm_lds_kernel<2, 2, 4, 4, EPI_QKV, 4, false, 16, true>), dim3(512 * 6), dim3(256), 0, s, a);
+            GemmArgs b = a0;
+            b.W = a0.W + (int64_t)768 * a0.K; b.N = 96; b.col_base = 768;
+            hipLaunchKernelGGL((gemm_lds_kernel<2, 2, 4, 3, EPI_QKV, 4, false, 16, true>), dim3(512), dim3(256), 0, s, b);
+        }};
+        for (int r = 0; r < 2; ++r)
+            run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true,
+                      {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), two, two4, GVAR(2, 2, 4, 4, EPI_QKV, 3, 16)}, rounds, iters);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "qkvepi") {  // what the QKV epilogue costs
