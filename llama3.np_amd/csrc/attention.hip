@@ -1,4 +1,6 @@
-// Fused causal attention dispatch (kernel template and design notes: attn_kernel.h).
+// Fused causal attention dispatch (kernel template and design notes: attn_kernel.h).  Every
+// launch takes the PK body (round 6: interleaved score chains, packed softmax pass; C3
+// 117.9-119.4 -> 116.3-116.7 us, the Llama-3 shape 829 -> 800 us, profiles/r06_attn_pk.txt)
 #include "attn_kernel.h"
 
 namespace l3 {
@@ -7,7 +9,7 @@ template <int HD, int QBW, int G, int KT>
 static hipError_t launch(const AttnArgs& a, hipStream_t s) {
     constexpr int QW = 16 * QBW * (4 / G);
     dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B), block(256);
-    hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT, true>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 
@@ -52,9 +54,9 @@ static hipError_t launch_last_hd(AttnArgs a, hipStream_t s) {
     const int QW = 16 * (4 / G);
     a.q_first = a.L > QW ? a.L - QW : 0;
     dim3 grid(1, a.H / G, a.B), block(256);
-    if (G == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 4, KT>), grid, block, 0, s, a);
-    else if (G == 2) hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, KT>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 1, KT>), grid, block, 0, s, a);
+    if (G == 4) hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 4, KT, true>), grid, block, 0, s, a);
+    else if (G == 2) hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 2, KT, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<HD, 1, 1, KT, true>), grid, block, 0, s, a);
     return hipGetLastError();
 }
 

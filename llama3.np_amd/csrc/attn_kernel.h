@@ -36,7 +36,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Timing-study variants of this kernel (ablation bits, the rejected DEFER schedule) live in
 // tools/attn_research.h, outside the product library.
-template <int HD, int QBW, int G, int KT>
+// PK (round 6, the product's launches; tools/attn_tune pk A/Bs it): the unmasked body's score chains interleaved over the
+// key groups (a d-group's four K fragments read together, one MFMA of each chain in turn) and
+// the softmax's subtract / sum on packed pairs (v_pk_add_f32: half the VALU ops of that pass);
+// the row sum then adds even and odd columns separately, so results differ in the last bits
+template <int HD, int QBW, int G, int KT, bool PK = false>
 __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
     static_assert(HD % 16 == 0 && KT % 16 == 0 && (G == 1 || G == 2 || G == 4), "shape");
     constexpr int WPH = 4 / G;                // waves per head
@@ -144,13 +148,31 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             for (int kg = 0; kg < KG; ++kg) {
                 live[kg] = !MASKED || (k0 + kg * 16) <= qmax_abs;     // wave-uniform
                 sacc[kg] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if (live[kg]) {
+            }
+            if constexpr (PK && !MASKED) {  // KG independent chains, one MFMA of each in turn
 #pragma unroll
-                    for (int dg = 0; dg < ND; ++dg) {
-                        const f32x4 kf = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
+                for (int dg = 0; dg < ND; ++dg) {
+                    f32x4 kf[KG];
 #pragma unroll
-                        for (int s = 0; s < 4; ++s)
-                            sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
+                    for (int kg = 0; kg < KG; ++kg)
+                        kf[kg] = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
+#pragma unroll
+                    for (int s = 0; s < 4; ++s)
+#pragma unroll
+                        for (int kg = 0; kg < KG; ++kg)
+                            sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[kg][s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int kg = 0; kg < KG; ++kg) {
+                    if (live[kg]) {
+#pragma unroll
+                        for (int dg = 0; dg < ND; ++dg) {
+                            const f32x4 kf = *reinterpret_cast<const f32x4*>(&Ks[cur][kg * 16 + fq][dg * 16 + fk]);
+#pragma unroll
+                            for (int s = 0; s < 4; ++s)
+                                sacc[kg] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qreg[j][dg][s], sacc[kg], 0, 0, 0);
+                        }
                     }
                 }
             }
@@ -175,14 +197,31 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(AttnArgs p) {
             const float alpha = __builtin_amdgcn_exp2f(m_run[j] - m_new);  // 0 on the first tile
             m_run[j] = m_new;
             float psum = 0.f;
+            if constexpr (PK) {
+                typedef float f32x2 __attribute__((ext_vector_type(2)));
+                const f32x2 mm = {m_new, m_new};
+                f32x2 ps = {0.f, 0.f};
 #pragma unroll
-            for (int kg = 0; kg < KG; ++kg)
+                for (int kg = 0; kg < KG; ++kg)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float pv = __builtin_amdgcn_exp2f(sacc[kg][r] - m_new);
-                    sacc[kg][r] = pv;
-                    psum += pv;
-                }
+                    for (int r = 0; r < 4; r += 2) {
+                        const f32x2 x = f32x2{sacc[kg][r], sacc[kg][r + 1]} - mm;
+                        const f32x2 e = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
+                        sacc[kg][r] = e.x;
+                        sacc[kg][r + 1] = e.y;
+                        ps += e;
+                    }
+                psum = ps.x + ps.y;
+            } else {
+#pragma unroll
+                for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float pv = __builtin_amdgcn_exp2f(sacc[kg][r] - m_new);
+                        sacc[kg][r] = pv;
+                        psum += pv;
+                    }
+            }
             l_run[j] = l_run[j] * alpha + psum;
 #pragma unroll
             for (int dg = 0; dg < ND; ++dg) o[j][dg] *= alpha;

@@ -36,6 +36,13 @@ struct Variant {
                 hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT>), grid, dim3(256), 0, s, a); \
             }}
 
+#define AVARPK(HD, QBW, G, KT)                                                                \
+    Variant{"attn<" #HD ",q" #QBW ",g" #G ",kt" #KT "> pk", [](const AttnArgs& a, hipStream_t s) { \
+                constexpr int QW = 16 * QBW * (4 / G);                                        \
+                dim3 grid((a.L + QW - 1) / QW, a.H / G, a.B);                                 \
+                hipLaunchKernelGGL((attn_fwd_kernel<HD, QBW, G, KT, true>), grid, dim3(256), 0, s, a); \
+            }}
+
 #define ADEF(HD, QBW, G, KT)                                                                  \
     Variant{"defer<" #HD ",q" #QBW ",g" #G ",kt" #KT ">", [](const AttnArgs& a, hipStream_t s) { \
                 constexpr int QW = 16 * QBW * (4 / G);                                        \
@@ -156,6 +163,14 @@ int main(int argc, char** argv) {
     }
     if (argc > 3 && std::string(argv[3]) == "stamps") {
         stamps(argc > 4 ? argv[4] : "gpurun_out/attn_stamps.bin", rounds);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "pk") {  // round 6: packed softmax + interleaved score chains
+        std::vector<Variant> v = {AVAR(48, 4, 1, 64), AVARPK(48, 4, 1, 64), AVAR(48, 4, 1, 64), AVARPK(48, 4, 1, 64)};
+        run("stories15M C3", 256, 256, 6, 6, 48, v, rounds, iters);
+        run("stories15M C3 half batch (one part of the split)", 128, 256, 6, 6, 48, v, rounds, iters);
+        run("Llama-3 shape B=2 L=2048 HD 128 GQA 4", 2, 2048, 32, 8, 128,
+            {AVAR(128, 1, 4, 32), AVARPK(128, 1, 4, 32)}, rounds, 3);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "c3") {  // the product C3 kernel alone (PMC passes)

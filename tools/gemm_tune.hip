@@ -284,10 +284,13 @@ static void stamp_report(const char* label, int M, int K, int N, bool norm) {
 // the first fragments' round trip, the rest of the k-loop, the wait at the partials' barrier,
 // the epilogue and its stores' acknowledgement.  All in 10 ns ticks of s_memrealtime.
 static int g_sk_ch = 2;
+static int g_sk_nw = 4;  // waves per block (the K split)
 template <int EPI, int TN>
 static void skinny_stamp_launch(GemmArgs g, hipStream_t s) {
     const int blocks = ((g.M + 15) / 16) * ((g.N + 16 * TN - 1) / (16 * TN));
-    if (g_sk_ch >= 6) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 6, 4, true>), dim3(blocks), dim3(256), 0, s, g);
+    if (g_sk_nw == 8) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2, 8, true>), dim3(blocks), dim3(512), 0, s, g);
+    else if (g_sk_nw == 16) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2, 16, true>), dim3(blocks), dim3(1024), 0, s, g);
+    else if (g_sk_ch >= 6) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 6, 4, true>), dim3(blocks), dim3(256), 0, s, g);
     else if (g_sk_ch >= 3) hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 3, 4, true>), dim3(blocks), dim3(256), 0, s, g);
     else hipLaunchKernelGGL((gemm_skinny_kernel<EPI, TN, 2, 4, true>), dim3(blocks), dim3(256), 0, s, g);
 }
@@ -374,8 +377,8 @@ static void skinny_stamps(int M, int reps) {
     }
     double tot = 0;
     for (int k = 0; k < 4; ++k) tot += (med(gap[k]) + med(span[k])) / 100;
-    printf("\n== skinny stamps M=%d CH=%d xcd-runs=%d: one layer's four launches %.2f us (us; medians over 6 layers' launches / their blocks; 10 ns ticks)\n",
-           M, g_sk_ch, (int)g_sk_xcd, tot);
+    printf("\n== skinny stamps M=%d CH=%d NW=%d xcd-runs=%d: one layer's four launches %.2f us (us; medians over 6 layers' launches / their blocks; 10 ns ticks)\n",
+           M, g_sk_ch, g_sk_nw, (int)g_sk_xcd, tot);
     for (int k = 0; k < 4; ++k)
         printf("   %-8s blocks %4d  gap from previous launch %.2f  span %.2f | per block: life %.2f = first fragments %.2f "
                "+ rest of k-loop %.2f + partials barrier %.2f + epilogue %.2f + stores acked %.2f\n",
@@ -384,6 +387,14 @@ static void skinny_stamps(int M, int reps) {
 }
 
 int main(int argc, char** argv) {
+    if (argc > 3 && std::string(argv[3]) == "skinnynw") {  // the K split over 4 / 8 / 16 waves
+        for (int r = 0; r < 2; ++r)
+            for (int nw : {4, 8, 16}) {
+                g_sk_nw = nw;
+                skinny_stamps(256, 20);
+            }
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "skinnystamps") {
         for (int r = 0; r < 2; ++r)
             for (int ch : {2, 3, 6})

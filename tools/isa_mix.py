@@ -44,7 +44,7 @@ def classify(op: str) -> str:
 
 def main():
     src = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "llama3.np_amd/csrc/attention.hip")
-    pat = sys.argv[2] if len(sys.argv) > 2 else "_ZN2l315attn_fwd_kernelILi48ELi4ELi1ELi64EEEvNS_8AttnArgsE"
+    pat = sys.argv[2] if len(sys.argv) > 2 else "_ZN2l315attn_fwd_kernelILi48ELi4ELi1ELi64ELb1EEEvNS_8AttnArgsE"
     with tempfile.TemporaryDirectory() as d:
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
                         "--save-temps", "-c", src, "-o", os.path.join(d, "k.o")], cwd=d, check=True,
