@@ -94,7 +94,8 @@ struct l3_ctx {
     static constexpr int MAX_PARTS = 4;
     hipStream_t aux[MAX_PARTS - 1] = {};
     hipEvent_t fork_ev = nullptr, join_ev[MAX_PARTS - 1] = {};
-    hipEvent_t lag_ev = nullptr;  // host path: the later parts' last layers wait for part 0's (forward_dev)
+    // host path: part p's last layers wait for part p - 1's same layer (forward_dev)
+    hipEvent_t lag_ev[MAX_PARTS - 1] = {};
     int split = 2;                   // parts (1 = off); l3_set_batch_split, L3_BATCH_SPLIT
     bool prune_last = true;          // last layer: attention / O-proj / FFN on the last rows only
                                      // (l3_set_last_layer_rows, L3_LAST_LAYER_ALL_ROWS)
@@ -421,12 +422,12 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     auto bail = [&](int rc) { l3_destroy(c); return rc; };
     if (set_dev(c)) return bail(1);
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->lag_ev, hipEventDisableTiming) != hipSuccess)
+        hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
         return bail(fail("hipStreamCreate / hipEventCreate failed"));
     for (int i = 0; i < l3_ctx::MAX_PARTS - 1; ++i)
         if (hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->lag_ev[i], hipEventDisableTiming) != hipSuccess)
             return bail(fail("hipStreamCreate / hipEventCreate failed"));
     c->layers.resize(d.n_layers > 0 ? d.n_layers : 0);
     if (d.n_layers > 0) {
@@ -506,7 +507,8 @@ extern "C" int l3_destroy(l3_ctx* c) {
         if (c->join_ev[i]) (void)hipEventDestroy(c->join_ev[i]);
     }
     if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-    if (c->lag_ev) (void)hipEventDestroy(c->lag_ev);
+    for (hipEvent_t e : c->lag_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -909,18 +911,19 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
     const int nl = (int)c->layers.size();
     // host path (logits_host): the logits copy is PCIe-bound (32.8 MB at C3, ~0.59 ms at 56 GB/s)
     // and can start only once a part's logits exist; in lockstep both parts reach their lm_heads
-    // together and the whole copy is exposed.  With lag k the later parts' last k layers each
-    // wait for part 0's same layer, so part 0 reaches its lm_head and starts its copy while the
-    // others still compute (L3_HOST_LAG; lockstep elsewhere: desynchronised parts pack worse)
+    // together and the whole copy is exposed.  With lag k part p's last k layers each wait for
+    // part p - 1's same layer (a staircase), so the earlier parts reach their lm_heads and start
+    // their copies while the later ones still compute (L3_HOST_LAG; lockstep elsewhere:
+    // desynchronised parts pack worse)
     const int host_lag_env = env_knob("L3_HOST_LAG", -1);
     const int lag = logits_host && parts > 1 ? (host_lag_env >= 0 ? host_lag_env : c->host_lag) : 0;
     for (int li = 0; li < nl && !rc; ++li) {
         roctxRangePushA(names[li < 8 ? li : 8]);
         for (int p = 0; p < parts && !rc; ++p) {
-            if (p > 0 && li >= nl - lag) HIP_TRY(hipStreamWaitEvent(st[p], c->lag_ev, 0));
+            if (p > 0 && li >= nl - lag) HIP_TRY(hipStreamWaitEvent(st[p], c->lag_ev[p - 1], 0));
             rc = run_layer(c, li, nb[p], L, start_pos, pos_dev, li == 0 ? ids_dev : nullptr, b0[p], st[p],
                            c->prune_last && li == nl - 1 && li > 0);
-            if (!rc && p == 0 && li >= nl - lag) HIP_TRY(hipEventRecord(c->lag_ev, st[0]));
+            if (!rc && p + 1 < parts && li >= nl - lag) HIP_TRY(hipEventRecord(c->lag_ev[p], st[p]));
         }
         roctxRangePop();
     }

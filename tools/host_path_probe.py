@@ -76,6 +76,17 @@ def main():
         os.environ["L3_HOST_LAG"] = str(k)
         res[f"lag{k}_bitwise_equal"] = bool(np.array_equal(m(ids, 0), x))
     os.environ.pop("L3_HOST_LAG", None)
+    # more batch parts on the host path (a staircase of lags: the last part's copy is smaller)
+    for rnd in range(2):
+        for parts, k in ((2, 2), (3, 2), (4, 2), (3, 1), (4, 1)):
+            ctx.set_batch_split(parts)
+            os.environ["L3_HOST_LAG"] = str(k)
+            res[f"host_path_parts{parts}_lag{k}_ms_r{rnd}"] = round(timeit(host, 20), 4)
+    for parts in (3, 4):
+        ctx.set_batch_split(parts)
+        res[f"forward_dev_parts{parts}_ms"] = round(timeit(dev, 10), 4)
+    os.environ.pop("L3_HOST_LAG", None)
+    ctx.set_batch_split(2)
     ctx.set_batch_split(1)
     res["forward_dev_split1_ms"] = round(timeit(dev, 10), 4)
     res["host_path_split1_ms"] = round(timeit(host, 10), 4)
