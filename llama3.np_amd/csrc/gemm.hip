@@ -265,12 +265,14 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     // Configurations chosen with tools/gemm_tune (interleaved A/B on MI355X).
     // 128 x 128 BK16: 120 VGPRs + 32 KB LDS -> 4 blocks per CU.
     const bool small_m = a.M <= 32;  // tiny M: 16 x 128 tile
-    // long K (the Llama-3 shape's gate|up): tiles in groups of 8 row tiles, so a k-step's
-    // concurrent blocks on an XCD share 8 A slices and ~12 W slices in L2 instead of one A slice
-    // and ~96 W slices (C5 gate|up 134.7 -> 135.8 TF/s, whole forward +0.3 %, bit-identical,
-    // profiles/r05_gemm_group_ab.txt; QKV -0.3 % and C3's K = 288 -0.4 % keep the row-major
-    // order); L3_GEMM_GROUP_M=0 turns it off (A/B)
-    static const int group_env = env_knob("L3_GEMM_GROUP_M", 8);
+    // long K (the Llama-3 shape's gate|up): tiles in groups of 4 row tiles walked column by
+    // column, so a k-step's concurrent blocks on an XCD share a few A and W slices in L2 instead
+    // of one A slice and ~96 W slices (round 5, groups of 8: C5 gate|up 134.7 -> 135.8 TF/s,
+    // profiles/r05_gemm_group_ab.txt; round 6 sweep, profiles/r06_c5_group_pmc.txt: 4 / 8 / 16 /
+    // 32 rows per group 136.6 / 135.9 / 134.6 / 128.6 TF/s and 222 / 261 / 264 / 474 GB of L2-miss
+    // traffic per launch; bit-identical; QKV and C3's K = 288 keep the row-major order);
+    // L3_GEMM_GROUP_M=0 turns it off (A/B)
+    static const int group_env = env_knob("L3_GEMM_GROUP_M", 4);
     GemmArgs ag = a;
     ag.group_m = a.K >= 1024 && !small_m ? group_env : 0;
     // EPI_QKV: the division-free full-tile epilogue (gemm_kernel.h qkv_epilogue_full) where its

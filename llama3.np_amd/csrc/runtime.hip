@@ -228,9 +228,6 @@ struct l3_ctx {
     // next decode entry point, before any further persistent step is launched
     bool persist_unsettled = false;
     int host_lag = 2;  // forward_dev: host-path lag of the later batch parts (layers; tools/host_path_probe.py)
-    // l3_forward_dev left its later batch parts un-joined (their work may still run on the aux
-    // streams); split_join makes the context stream wait for them (join_ev) before anything else
-    int split_pending = 0, split_B = 0, split_L = 0;  // ... and the row layout it left them on
     int64_t persist_recoveries = 0;  // steps recovered on the graph path (stats)
     hipEvent_t order_ev = nullptr;   // after this context's last decode graph (launch_decode_graph)
 };
@@ -238,16 +235,8 @@ struct l3_ctx {
 // ---------------------------------------------------------------------------------------
 // join = the context stream waits for an in-flight logits gather: every entry point except
 // l3_forward_dev (which waits only before its lm_head) and the gather itself
-// the later batch parts of a device-resident forward, if it left them un-joined (split_pending)
-static int split_join(l3_ctx* c) {
-    for (int p = 1; p < c->split_pending; ++p) HIP_TRY(hipStreamWaitEvent(c->stream, c->join_ev[p - 1], 0));
-    c->split_pending = 0;
-    return 0;
-}
-
 static int set_dev(l3_ctx* c, bool join = true) {
     HIP_TRY(hipSetDevice(c->device));
-    if (join && split_join(c)) return 1;
     if (join) c->gather_tail = false;
     if (join && c->gather_pending) {
         HIP_TRY(hipStreamWaitEvent(c->stream, c->comm_done_ev, 0));
@@ -317,7 +306,6 @@ static void drop_decode_graph(l3_ctx* c) {
 static int ensure_ws(l3_ctx* c, int64_t B, int64_t L) {
     const int64_t T = B * L;
     if (T <= c->ws_T && B <= c->ws_B) return 0;
-    if (split_join(c)) return 1;  // a part still running reads the buffers freed below
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->gather_tail = false;
     drop_decode_graph(c);  // the captured graph holds workspace pointers
@@ -882,7 +870,7 @@ static int fold_parts(l3_ctx* c, int B) {
 // host_pitch * r (the group's interleave, one 2-D copy per part over this member's own link)
 static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int start_pos,
                        float* logits_dev, const int* pos_dev = nullptr, float* logits_host = nullptr,
-                       int host_pitch = 1, int host_off = 0, bool defer_join = false) {
+                       int host_pitch = 1, int host_off = 0) {
     // roctx ranges (host-side launch spans; `rocprofv3 --marker-trace`) per block and lm_head
     static const char* names[] = {"l3.layer0", "l3.layer1", "l3.layer2", "l3.layer3", "l3.layer4",
                                   "l3.layer5", "l3.layer6", "l3.layer7", "l3.layerN"};
@@ -902,11 +890,6 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
         nb[p] = (int)((int64_t)B * (p + 1) / parts) - b0[p];
         st[p] = p ? c->aux[p - 1] : c->stream;
     }
-    // parts a previous device-resident forward left running: this forward's part p may overlap
-    // them only where it rewrites exactly their rows (same parts, B and L); otherwise join first
-    if (c->split_pending &&
-        !(defer_join && parts == c->split_pending && B == c->split_B && L == c->split_L) && split_join(c))
-        return 1;
     roctxRangePushA("l3.forward");
     // a logits gather queued last on stream (mode 3): the other parts start from the point just
     // before it, so their layers overlap the transfer; part 0 runs after it on stream, and every
@@ -970,19 +953,9 @@ static int forward_dev(l3_ctx* c, const int32_t* ids_dev, int B, int L, int star
         if (!rc) rc = d2h_rows(b0[p], nb[p], st[p]);
     }
     roctxRangePop();
-    // stream waits for every part: later calls see all rows.  defer_join (l3_forward_dev, device-
-    // resident logits): the wait is left to the next call that needs it (split_join: every entry
-    // point but l3_forward_dev, the gather, a workspace regrowth), so the next device-resident
-    // forward's part 0 starts behind part 0 only and its first layer fills the GPU during the
-    // later parts' last-layer tail (the last-position chain and lm_head: few blocks)
-    for (int p = 1; p < parts; ++p) {
+    for (int p = 1; p < parts; ++p) {  // stream waits for every part: later calls see all rows
         HIP_TRY(hipEventRecord(c->join_ev[p - 1], st[p]));
-        if (!defer_join || !lm_parts) HIP_TRY(hipStreamWaitEvent(c->stream, c->join_ev[p - 1], 0));
-    }
-    if (defer_join && lm_parts && parts > 1) {
-        c->split_pending = parts;
-        c->split_B = B;
-        c->split_L = L;
+        HIP_TRY(hipStreamWaitEvent(c->stream, c->join_ev[p - 1], 0));
     }
     roctxRangePushA("l3.lm_head");
     if (!rc && !lm_parts) {
@@ -1061,9 +1034,7 @@ extern "C" int l3_forward_dev(l3_ctx* c, const int32_t* ids_dev, int32_t B, int3
     CHECK_CTX(c);
     if (need_model(c) || check_call(c, B, L, start_pos) || set_dev(c, false) || spec_resolve(c) || ensure_ws(c, B, L))
         return 1;
-    // L3_SPLIT_NOJOIN=0: join the batch parts at the end of every call (A/B)
-    static const bool nojoin = env_knob("L3_SPLIT_NOJOIN", 1) != 0;
-    return forward_dev(c, ids_dev, B, L, start_pos, logits_dev, nullptr, nullptr, 1, 0, nojoin);
+    return forward_dev(c, ids_dev, B, L, start_pos, logits_dev);
 }
 
 extern "C" int l3_forward_host(l3_ctx* c, const int64_t* ids_host, int32_t B, int32_t L,
@@ -2161,7 +2132,7 @@ extern "C" int l3_comm_gather_logits(l3_ctx* c, const float* src_dev, float* dst
     if (c->group) return fail("l3_comm_gather_logits: this context is a member of an l3_group (use l3_group_*)");
     if (check_rows(c, "l3_comm_gather_logits", rows_per_rank, root)) return 1;
     if (c->rank == root && !dst_dev) return fail("l3_comm_gather_logits: null destination on the root");
-    if (set_dev(c, false) || split_join(c)) return 1;  // every part's rows are written
+    if (set_dev(c, false)) return 1;
     const int64_t VS = c->d.vocab_size;
     // Mode 1 (default): on the context stream, after the forward that wrote src and before the next one —
     // no cross-stream events, the transfer fully serialized.  The overlapped form (mode 0: the

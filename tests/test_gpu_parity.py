@@ -354,48 +354,6 @@ def test_sharded_prefill_world1_rccl(tmpdir_mod):
     np.testing.assert_array_equal(nxt[:, 0], np.argmax(want[:, 0, :], axis=-1))
 
 
-def test_forward_dev_deferred_join(tmpdir_mod):
-    """l3_forward_dev leaves its later batch parts un-joined (runtime.hip split_pending): the next
-    device-resident forward's part 0 starts behind part 0 only.  Back-to-back forwards into
-    separate logits buffers, then a forward with another row layout (B, L, the batch split) that
-    must join first, then reads through d2h, a host forward and a greedy step (entry points that
-    join): every buffer holds its own forward's logits, bit-identical to Llama.__call__
-    (llama3.py:285-308; rows never interact, :163-211)."""
-    # B > 128 per part pair: every part takes the batch's lm_head tile, so the lm_heads run per
-    # part and the forward may defer its join (runtime.hip forward_dev lm_parts)
-    args = synth.stories15m(256)
-    _, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
-    VS = args.vocab_size
-    rng = np.random.default_rng(77)
-    shapes = [(256, 32), (256, 32), (256, 32), (200, 32), (256, 24), (256, 32)]
-    ids = [rng.integers(0, VS, sh).astype(np.int32) for sh in shapes]
-    ref = llama3.Llama(path, args)
-    want = [ref(x, 0)[:, 0, :] for x in ids]
-    m = llama3.Llama(path, args)
-    ctx = m.context
-    ctx.set_batch_split(2, min_tokens=1)
-    ids_dev = [ctx.alloc(x.nbytes) for x in ids]
-    for d, x in zip(ids_dev, ids):
-        ctx.h2d(d, x)
-    bufs = [ctx.alloc(x.shape[0] * VS * 4) for x in ids]
-    for k, x in enumerate(ids):
-        if k == 5:
-            ctx.set_batch_split(3, min_tokens=1)  # another part layout: joins first
-        ctx.forward_dev(ids_dev[k], x.shape[0], x.shape[1], 0, bufs[k])
-    got = [ctx.d2h(np.empty((x.shape[0], VS), np.float32), b) for x, b in zip(ids, bufs)]
-    for k, (g, w) in enumerate(zip(got, want)):
-        np.testing.assert_array_equal(g, w, err_msg=f"forward {k}")
-    # a device-resident forward, then at once a host forward and a greedy step on other rows
-    ctx.set_batch_split(2, min_tokens=1)
-    ctx.forward_dev(ids_dev[0], 256, 32, 0, bufs[0])
-    np.testing.assert_array_equal(m(ids[1].astype(np.int64), 0)[:, 0, :], want[1])
-    ctx.forward_dev(ids_dev[2], 256, 32, 0, bufs[2])
-    nxt, _ = ctx.greedy_step(ids[0].astype(np.int64), 0)
-    np.testing.assert_array_equal(nxt, want[0].argmax(-1))
-    np.testing.assert_array_equal(ctx.d2h(np.empty((256, VS), np.float32), bufs[2]), want[2])
-    ctx.set_batch_split(2)
-
-
 @pytest.mark.parametrize("overlap", [False, True])
 def test_gather_pipelined_forwards_world1(tmpdir_mod, overlap):
     """Forwards and gathers queued back to back on one logits buffer, as bench.py does — the
