@@ -646,6 +646,10 @@ def main():
         bpg = B_PER_GPU
     N = dist.world
     dev = dist.local_rank
+    # a launcher that shows each rank only its own GPU (HIP_VISIBLE_DEVICES per rank): that GPU
+    # is device 0 here (check_devices still proves N distinct devices over RCCL)
+    if not a.single_process and dev > 0 and dev >= l3hip.device_count():
+        dev = 0
     args = synth.stories15m(bpg)
     FD, D = synth.STORIES15M_HIDDEN, args.dim
     weights = synth.make_weights(args, FD, seed=0)

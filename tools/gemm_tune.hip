@@ -627,6 +627,18 @@ int main(int argc, char** argv) {
         }
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "normab") {  // the two norm-fused C3 GEMMs (run by gemm_tune and gemm_tune_ssh)
+        Variant fast{"QKV glds<2,2,4,3,wpe4,bk16> fast epilogue", [](const GemmArgs& a0, hipStream_t s) {
+            GemmArgs a = a0;
+            a.qkv_fast = true;
+            hipLaunchKernelGGL((gemm_lds_kernel<2, 2, 4, 3, EPI_QKV, 4, false, 16, true>), dim3(512 * 9), dim3(256), 0, s, a);
+        }};
+        for (int r = 0; r < 2; ++r) {
+            run_shape("QKV (+RoPE, KV append)", EPI_QKV, M, 288, 864, true, {fast}, rounds, iters);
+            run_shape("gate|up (SwiGLU)", EPI_SWIGLU, M, 288, 1536, true, {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16)}, rounds, iters);
+        }
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "qkvsplit") {  // round 6: QKV columns by two tiles
         // columns [0, 768) on the 128 x 128 tile (16 MFMAs per 4-deep k-step, the gate|up tile:
         // 6 column tiles, no padding) and [768, 864) on 128 x 96, as two launches
