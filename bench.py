@@ -54,6 +54,9 @@ import synth  # noqa: E402
 
 METRIC = "tokens/s stories15M batch-256 seq-256 prefill; % fp32 MFMA peak on FFN GEMM"
 PEAK_FP32_TFLOPS = 157.3  # MI355X dense fp32 MFMA (MI355X_MICROARCH.md)
+# the x6 path's ceiling in fp32-equivalent FLOP/s: the dense bf16 MFMA peak (256 CUs x 4 SIMDs x
+# 1024 FLOP/clk x 2.4 GHz = 2516.6 TF/s, MI355X_MICROARCH.md) over its six products per fp32 one
+PEAK_X6_TFLOPS = round(2516.6 / 6, 1)
 B_PER_GPU, SEQ = 256, 256
 
 
@@ -620,6 +623,8 @@ def main():
                          "part runs during the gather (default: serialized)")
     ap.add_argument("--spawn-timeout", type=float, default=1800.0,
                     help="seconds before spawned ranks still running are killed (0: no limit)")
+    ap.add_argument("--no-x6", action="store_true",
+                    help="skip the beside-value pass of the opt-in x6 GEMM path (l3_set_gemm_x6)")
     ap.add_argument("--spawn", action="store_true",
                     help="start the rank processes here even at N=1 (rehearses the launcher-free "
                          "N>1 path; N>1 without WORLD_SIZE spawns anyway)")
@@ -766,6 +771,32 @@ def main():
     each(lambda m: m.set_batch_split(a.split if a.split is not None else 2))
     each(lambda m: m.set_last_layer_rows(False))
 
+    # beside `value`: the opt-in x6 GEMM path (l3_set_gemm_x6: the prefill projections from six
+    # bf16 MFMA products per fp32 product, gemm_x6.h) on the same steps, its gate|up launch time
+    # from a serialized event pass, and its logits against the fp32 path's (never `value`)
+    x6 = None
+    if not a.no_x6:
+        ref_logits = np.empty((bpg, VS), np.float32)
+        ctx.d2h(ref_logits, logits_dev)  # the fp32 path's last step (same ids every step)
+        each(lambda m: m.set_gemm_x6(True))
+        for _ in range(a.warmup):
+            step()
+        x6_elapsed, _ = timed_steps(a.steps)
+        x6_logits = np.empty((bpg, VS), np.float32)
+        ctx.d2h(x6_logits, logits_dev)
+        each(lambda m: m.set_last_layer_rows(True))
+        each(lambda m: m.set_batch_split(1))
+        step()
+        ctx.kernel_timing(True, ["gateup", "down"])
+        timed_steps(a.steps)
+        x6_stats = ctx.kernel_stats()
+        ctx.kernel_timing(False)
+        each(lambda m: m.set_batch_split(a.split if a.split is not None else 2))
+        each(lambda m: m.set_last_layer_rows(False))
+        each(lambda m: m.set_gemm_x6(False))
+        x6 = (x6_elapsed, x6_stats, float(np.abs(x6_logits - ref_logits).max()),
+              int((x6_logits.argmax(1) == ref_logits.argmax(1)).sum()))
+
     # N > 1: the logits gather alone (untimed for `value`): its share of a step at this N,
     # which the overlapped gather hides behind the next step's layers
     gather_ms = None
@@ -873,6 +904,29 @@ def main():
                      "ffn": {"achieved": round(ffn_tf, 2),
                              "frac": round(ffn_tf / PEAK_FP32_TFLOPS, 4)}},
     }
+    if x6 is not None:
+        x6_elapsed, x6_stats, x6_diff, x6_same = x6
+        gu6_ms, gu6_n = x6_stats["gateup"]
+        dn6_ms, dn6_n = x6_stats["down"]
+        gu6 = gu_flops / (gu6_ms / gu6_n / 1e3) / 1e12
+        ffn6 = (gu_flops + dn_flops) / ((gu6_ms / gu6_n + dn6_ms / dn6_n) / 1e3) / 1e12
+        out["gemm_x6"] = {
+            "what": "opt-in path (l3_set_gemm_x6 / L3_GEMM_X6=1): QKV / O-proj / gate|up / down from "
+                    "six bf16 MFMA products per fp32 product (operands cut exactly into three bf16 "
+                    "pieces; gemm_x6.h); attention and lm_head fp32; same steps and timing as value",
+            "value": round(tokens / x6_elapsed, 1), "unit": "tokens/s",
+            "ms_per_step": round(x6_elapsed / a.steps * 1e3, 4),
+            "logits_max_abs_diff_vs_fp32_path": x6_diff,
+            "argmax_rows_equal_vs_fp32_path": f"{x6_same}/{bpg}",
+            "whole_step_fp32_equivalent_tflops": round(fl_pruned * a.steps / x6_elapsed / 1e12, 2),
+            "roofline": {"kernel": f"x6 gemm gate|up (fused SwiGLU epilogue), M={T} K=288 N=1536",
+                         "bound": "mfma", "achieved": round(gu6, 2), "peak": PEAK_X6_TFLOPS,
+                         "unit": "fp32-equivalent TFLOP/s (6 bf16 MFMA per fp32 product)",
+                         "frac": round(gu6 / PEAK_X6_TFLOPS, 4),
+                         "bf16_mfma_tflops_executed": round(6 * gu6, 1),
+                         "vs_fp32_mfma_peak": round(gu6 / PEAK_FP32_TFLOPS, 4),
+                         "ffn": {"achieved": round(ffn6, 2), "frac": round(ffn6 / PEAK_X6_TFLOPS, 4)}},
+        }
     if dist.world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if dist.world == 1 and not a.no_kernel_breakdown:

@@ -124,6 +124,15 @@ int l3_set_batch_split(l3_ctx* ctx, int32_t parts, int64_t min_tokens);
  * (tests: <= 1e-5 against the all-rows logits, C smoke 1e-4).  all_rows != 0: every position
  * through the whole block. */
 int l3_set_last_layer_rows(l3_ctx* ctx, int32_t all_rows);
+/* GEMM arithmetic of the prefill projections (extension; default off, env L3_GEMM_X6=1 turns it
+ * on for new contexts).  on != 0: the QKV / O-proj / gate|up / down GEMMs past 32 rows run on the
+ * x6 kernel — each fp32 operand cut exactly into three bf16 pieces and the product summed from
+ * the six largest piece products on bf16 MFMAs (gemm_x6.h; error against an fp64 product at or
+ * below the fp32 MFMA kernel's, tools/gemm_tune x6acc) — with 1.5x the layer weights' memory for
+ * the pieces, made now (or at l3_finalize).  Results round differently from the fp32 MFMA path
+ * (not bit-identical to it); batch-1 / batched decode (<= 256 rows), the lm_head and the
+ * attention keep their fp32 kernels.  on == 0 frees the pieces. */
+int l3_set_gemm_x6(l3_ctx* ctx, int32_t on);
 /* Same with device-resident ids (int32 [B, L]) and logits ([B, VS]); async. */
 int l3_forward_dev(l3_ctx* ctx, const int32_t* ids_dev, int32_t B, int32_t L,
                    int32_t start_pos, float* logits_dev);

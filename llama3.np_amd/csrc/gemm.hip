@@ -3,6 +3,7 @@
 #include <cstdlib>
 
 #include "gemm_kernel.h"
+#include "gemm_x6.h"
 
 namespace l3 {
 
@@ -15,6 +16,23 @@ static hipError_t launch(const GemmArgs& a, hipStream_t s) {
     const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
     hipLaunchKernelGGL((gemm_lds_kernel<WM, WN, TM, TN, EPI, WPE, false, BK, true, NS>),
                        dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a);
+    return hipGetLastError();
+}
+
+// the opt-in x6 path (gemm_x6.h): six bf16 MFMA products per fp32 product, W3 pieces from
+// l3_finalize; 64 x WN*TN*16 ... tiles chosen with tools/gemm_tune x6
+template <int EPI, int WM, int WN, int TM, int TN>
+static hipError_t launch_x6(const GemmArgs& a, hipStream_t s) {
+    constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
+    const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+    hipLaunchKernelGGL((gemm_x6_kernel<WM, WN, TM, TN, EPI, 2>), dim3((unsigned)tiles), dim3(64 * WM * WN), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_planes(const float* w, unsigned short* w3, int64_t rows, int K, hipStream_t s) {
+    const int64_t n = rows * K;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, w, w3, rows, K);
     return hipGetLastError();
 }
 
@@ -280,6 +298,18 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     // sequences; L3_QKV_FAST_EPI=0 keeps the generic epilogue (A/B; both round identically)
     static const bool qkv_fast_env = env_knob("L3_QKV_FAST_EPI", 1) != 0;
     ag.qkv_fast = epi == EPI_QKV && qkv_fast_env && a.HD % 16 == 0 && a.L >= 64;
+    if (a.W3 && !small_m && epi != EPI_STORE) {  // x6 (opt-in): 128-row tiles of four waves
+        switch (epi) {
+            case EPI_SWIGLU: return launch_x6<EPI_SWIGLU, 4, 1, 2, 8>(ag, s);   // 128 x 128
+            case EPI_QKV:
+                if (a.N % 96 == 0) return launch_x6<EPI_QKV, 4, 1, 2, 6>(ag, s);  // 128 x 96
+                return launch_x6<EPI_QKV, 4, 1, 2, 8>(ag, s);
+            case EPI_RESID:
+                if (a.N % 96 == 0) return launch_x6<EPI_RESID, 4, 1, 2, 6>(ag, s);
+                return launch_x6<EPI_RESID, 4, 1, 2, 8>(ag, s);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (epi) {
         case EPI_SWIGLU:  // 128 x 128, BK 16
             if (small_m) return launch<EPI_SWIGLU, 1, 4, 1, 2, 2, 32>(a, s);

@@ -81,6 +81,8 @@ struct DecState {
 struct GemmArgs {
     const float* A; int64_t lda;   // A rows, row stride (floats)
     const float* W;                // [N, K] row-major
+    const unsigned short* W3;      // opt-in x6 path (gemm_x6.h): W as three bf16 pieces
+                                   // [N][3][K] (null: the fp32 MFMA kernels)
     float* C; int64_t ldc;         // output (EPI_QKV: unused)
     int M, N, K;
     bool norm;                     // RMSNorm on A: rows scaled by 1/sqrt(mean(A^2)+eps); the norm
@@ -343,6 +345,8 @@ int decode_persist_grid(const DecodePersistArgs& a);
 hipError_t launch_decode_persist(const DecodePersistArgs& a, int grid, hipStream_t s);
 
 hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s);
+// W [rows][K] fp32 -> W3 [rows][3][K] bf16 pieces for the x6 path (gemm_x6.h)
+hipError_t launch_split_planes(const float* w, unsigned short* w3, int64_t rows, int K, hipStream_t s);
 hipError_t launch_attention(const AttnArgs& a, hipStream_t s);
 hipError_t launch_attention_last(const AttnArgs& a, hipStream_t s);
 hipError_t launch_argmax(const float* logits, int64_t rows, int n, int32_t* out, hipStream_t s,

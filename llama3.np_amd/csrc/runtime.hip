@@ -78,6 +78,9 @@ struct Layer {
     unsigned have = 0;  // bitmask of uploaded kinds
     // RMSNorm weight folded into the consuming GEMM's W columns at l3_finalize
     bool folded_qkv = false, folded_gu = false;
+    // the opt-in x6 GEMM path (gemm_x6.h, l3_set_gemm_x6): each weight as three bf16 pieces
+    // [N][3][K], made from the folded fp32 weight (null when the path is off)
+    unsigned short *wqkv3 = nullptr, *wo3 = nullptr, *wgu3 = nullptr, *wd3 = nullptr;
 };
 
 struct Timer {
@@ -97,6 +100,7 @@ struct l3_ctx {
     // host path: part p's last layers wait for part p - 1's same layer (forward_dev)
     hipEvent_t lag_ev[MAX_PARTS - 1] = {};
     int split = 2;                   // parts (1 = off); l3_set_batch_split, L3_BATCH_SPLIT
+    bool gemm_x6 = false;            // prefill GEMMs on the x6 path (l3_set_gemm_x6, L3_GEMM_X6)
     bool prune_last = true;          // last layer: attention / O-proj / FFN on the last rows only
                                      // (l3_set_last_layer_rows, L3_LAST_LAYER_ALL_ROWS)
     int64_t split_min_tokens = 8192; // a part must hold at least this many tokens
@@ -411,6 +415,7 @@ extern "C" int l3_create(int32_t device, const l3_dims* dims, l3_ctx** out) {
     c->device = device;
     c->d = d;
     c->prune_last = env_knob("L3_LAST_LAYER_ALL_ROWS", 0) == 0;
+    c->gemm_x6 = env_knob("L3_GEMM_X6", 0) != 0;
     {  // batch-split default for new contexts
         const int n = env_knob("L3_BATCH_SPLIT", c->split);
         c->split = n < 1 ? 1 : n > l3_ctx::MAX_PARTS ? l3_ctx::MAX_PARTS : n;
@@ -477,6 +482,7 @@ extern "C" int l3_destroy(l3_ctx* c) {
     for (auto& L : c->layers) {
         dfree(L.wqkv); dfree(L.wo); dfree(L.wgu); dfree(L.wd); dfree(L.n_attn); dfree(L.n_ffn);
         dfree(L.cache_k); dfree(L.cache_v);
+        dfree(L.wqkv3); dfree(L.wo3); dfree(L.wgu3); dfree(L.wd3);
     }
     dfree(c->emb); dfree(c->lm_head); dfree(c->final_norm); dfree(c->rope_cos); dfree(c->rope_sin);
     dfree(c->h); dfree(c->q); dfree(c->attn); dfree(c->hid); dfree(c->logits); dfree(c->ids);
@@ -596,6 +602,45 @@ static const unsigned NEED_ATTN = (1u << L3_W_Q) | (1u << L3_W_K) | (1u << L3_W_
 static const unsigned NEED_LAYER = NEED_ATTN | (1u << L3_W_GATE) | (1u << L3_W_UP) |
                                    (1u << L3_W_DOWN) | (1u << L3_W_ATTN_NORM) | (1u << L3_W_FFN_NORM);
 
+// the x6 pieces of every layer weight (gemm_x6.h), from the weights as the GEMMs use them
+// (after the RMSNorm fold); free_x6 drops them
+static void free_x6(l3_ctx* c) {
+    for (auto& L : c->layers) {
+        dfree(L.wqkv3); dfree(L.wo3); dfree(L.wgu3); dfree(L.wd3);
+        L.wqkv3 = L.wo3 = L.wgu3 = L.wd3 = nullptr;
+    }
+}
+
+static int make_x6(l3_ctx* c) {
+    const int64_t D = c->d.dim, FD = c->d.hidden_dim;
+    for (auto& L : c->layers) {
+        if (L.wqkv3) continue;
+        if (hipMalloc(&L.wqkv3, c->qkvn * D * 6) || hipMalloc(&L.wo3, D * c->qdim * 6) ||
+            hipMalloc(&L.wgu3, 2 * FD * D * 6) || hipMalloc(&L.wd3, D * FD * 6)) {
+            free_x6(c);
+            return fail("l3_set_gemm_x6: out of device memory (1.5x the layer weights)");
+        }
+        HIP_TRY(launch_split_planes(L.wqkv, L.wqkv3, c->qkvn, (int)D, c->stream));
+        HIP_TRY(launch_split_planes(L.wo, L.wo3, D, c->qdim, c->stream));
+        HIP_TRY(launch_split_planes(L.wgu, L.wgu3, 2 * FD, (int)D, c->stream));
+        HIP_TRY(launch_split_planes(L.wd, L.wd3, D, (int)FD, c->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int l3_set_gemm_x6(l3_ctx* c, int32_t on) {
+    CHECK_CTX(c);
+    if (set_dev(c)) return 1;
+    c->gemm_x6 = on != 0;
+    if (!c->gemm_x6) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        free_x6(c);
+        return 0;
+    }
+    return c->finalized ? make_x6(c) : 0;  // else l3_finalize makes them
+}
+
 extern "C" int l3_finalize(l3_ctx* c) {
     CHECK_CTX(c);
     if (c->finalized) return 0;
@@ -622,6 +667,7 @@ extern "C" int l3_finalize(l3_ctx* c) {
         c->folded_lm = true;
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->gemm_x6 && make_x6(c)) return 1;
     c->finalized = true;
     return 0;
 }
@@ -727,7 +773,11 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     // a pruned block with more than 256 rows (the tiled QKV kernel): K / V for every row, q for
     // the last row of each sequence only (its RoPE at position start_pos + L - 1)
     const bool kv_only = prune && T > 256;
-    if (kv_only) { g.W = Ly.wqkv + (int64_t)c->qdim * D; g.N = 2 * c->kvdim; g.col_base = c->qdim; }
+    g.W3 = Ly.wqkv3;  // null unless the x6 path is on (then launch_gemm takes it past 32 rows)
+    if (kv_only) {
+        g.W = Ly.wqkv + (int64_t)c->qdim * D; g.N = 2 * c->kvdim; g.col_base = c->qdim;
+        if (g.W3) g.W3 += (int64_t)c->qdim * 3 * D;
+    }
     if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, g, s); })) return 1;
     if (prune) {
         const int D4 = D;
@@ -738,7 +788,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
         GemmArgs o{};  // O-proj + residual on the last rows, in place on h
         if (kv_only) {
             GemmArgs gq = g;  // q of the last rows: [B, qdim], compact
-            gq.A = hl; gq.lda = (int64_t)L * D4; gq.W = Ly.wqkv; gq.N = c->qdim; gq.col_base = 0;
+            gq.A = hl; gq.lda = (int64_t)L * D4; gq.W = Ly.wqkv; gq.W3 = nullptr; gq.N = c->qdim; gq.col_base = 0;
             gq.M = B; gq.L = 1; gq.start_pos = start_pos + L - 1; gq.force_skinny = true;
             gq.ws = nullptr;
             if (timed_on(c, L3_K_QKV, s, [&] { return launch_gemm(EPI_QKV, gq, s); })) return 1;
@@ -763,11 +813,11 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
         return timed_on(c, L3_K_DOWN, s, [&] { return launch_gemm(EPI_RESID, dl, s); });
     }
     GemmArgs gu{};  // rmsnorm -> gate|up -> SwiGLU
-    gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.C = hid; gu.ldc = FD;
+    gu.A = h; gu.lda = D; gu.W = Ly.wgu; gu.W3 = Ly.wgu3; gu.C = hid; gu.ldc = FD;
     gu.M = (int)T; gu.N = 2 * FD; gu.K = D; gu.norm = true;  // n_ffn folded into wgu
     gu.eps = c->d.norm_eps;
     GemmArgs dn{};  // down + residual
-    dn.A = hid; dn.lda = FD; dn.W = Ly.wd; dn.C = h; dn.ldc = D;
+    dn.A = hid; dn.lda = FD; dn.W = Ly.wd; dn.W3 = Ly.wd3; dn.C = h; dn.ldc = D;
     dn.M = (int)T; dn.N = D; dn.K = FD; dn.norm = false;
     gu.ws = dn.ws = skws; gu.ws_cap = dn.ws_cap = c->skws_cap;
     // Batch-1 decode: the O-proj rides in the attention launch as per-head partial rows, which
@@ -794,7 +844,7 @@ static int run_layer(l3_ctx* c, int li, int B, int L, int start_pos, const int* 
     } else {
         // O-proj + residual (in place on h)
         GemmArgs o{};
-        o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.C = h; o.ldc = D;
+        o.A = attn; o.lda = c->qdim; o.W = Ly.wo; o.W3 = Ly.wo3; o.C = h; o.ldc = D;
         o.M = (int)T; o.N = D; o.K = c->qdim; o.norm = false;
         o.ws = skws; o.ws_cap = c->skws_cap;
         if (emb_ids) { o.res_src = c->emb; o.res_rows = emb_ids; }  // h = emb[ids] + attn . Wo^T

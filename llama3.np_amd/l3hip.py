@@ -78,6 +78,7 @@ _SIGNATURES = {
     "l3_d2h": (ctypes.c_int, [_P, _P, _P, _SZ]),
     "l3_synchronize": (ctypes.c_int, [_P]),
     "l3_set_batch_split": (ctypes.c_int, [_P, _I32, _I64]),
+    "l3_set_gemm_x6": (ctypes.c_int, [_P, _I32]),
     "l3_set_last_layer_rows": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_timing": (ctypes.c_int, [_P, _I32]),
     "l3_kernel_stats": (ctypes.c_int, [_P, _P, _P]),
@@ -362,6 +363,12 @@ class Context:
         """Extension: False (default) runs the last block's attention / O-proj / FFN on each
         sequence's last position only (l3_set_last_layer_rows); True, every position."""
         check(lib().l3_set_last_layer_rows(self._h, int(bool(all_rows))))
+
+    def set_gemm_x6(self, on: bool) -> None:
+        """Extension (l3_set_gemm_x6): the prefill projections on the x6 kernel — fp32 operands
+        cut exactly into three bf16 pieces, six bf16 MFMA products per fp32 product (error
+        against fp64 at or below the fp32 MFMA kernel's); off (default) frees the pieces."""
+        check(lib().l3_set_gemm_x6(self._h, int(bool(on))))
 
     def synchronize(self) -> None:
         check(lib().l3_synchronize(self._h))

@@ -1288,3 +1288,72 @@ def test_generate_schedule_edges(tmpdir_mod, monkeypatch, persist):
             got = m.generate_all(p, n) if k % 2 else np.concatenate(list(m.generate(p, n)) or [np.empty((B, 0), np.int64)], axis=1)
             assert got.shape == want.shape, (k, got.shape, want.shape)
             np.testing.assert_array_equal(got, want, err_msg=f"B={B} call {k}: L={p.shape[1]} max_new={n}")
+
+
+# ---- round 6: the opt-in x6 GEMM path (l3_set_gemm_x6, gemm_x6.h) -------------------------
+# The prefill projections past 32 rows from six bf16 MFMA products per fp32 product (operands cut
+# exactly into three bf16 pieces).  Not bit-identical to the fp32 MFMA path; held to the same
+# bars against the oracle: 1e-4 max-abs (default weights), the reference's rtol form (sharp),
+# greedy ids exact.  Batch-1 / <= 256-row decode keeps the fp32 kernels, so the generate tests
+# exercise x6 through their > 256-token prefills.
+
+def test_x6_c3_rows_match_oracle_and_split(tmpdir_mod):
+    """C3 shape (B = 256, L = 256) on the x6 path: 16 spread rows against the oracle (1e-4),
+    every row's argmax equal to the fp32 path's, the batch split bit-identical to one part (the
+    x6 kernel's per-element arithmetic does not depend on M or the tile), and switching the
+    path off gives the fp32 path's logits bit for bit."""
+    args = synth.stories15m(256)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 0, "default")
+    m = llama3.Llama(path, args)
+    ids = np.random.default_rng(1).integers(0, args.vocab_size, (256, 256))
+    f32 = m(ids, 0)
+    m.context.set_gemm_x6(True)
+    x6 = m(ids, 0)
+    assert np.isfinite(x6).all()
+    assert np.abs(x6 - f32).max() <= 1e-4
+    np.testing.assert_array_equal(x6.argmax(-1), f32.argmax(-1))
+    rows = [0, 1, 15, 16, 63, 64, 100, 127, 128, 129, 131, 191, 200, 239, 254, 255]
+    ref = orc.OracleModel(w, synth.stories15m(len(rows)))
+    assert _close(x6[rows], ref(ids[rows], 0)) <= 1e-4
+    m.context.set_batch_split(1)
+    np.testing.assert_array_equal(m(ids, 0), x6)
+    m.context.set_batch_split(2)
+    m.context.set_gemm_x6(False)
+    np.testing.assert_array_equal(m(ids, 0), f32)
+
+
+def test_x6_live_oracle_sharp_and_greedy(tmpdir_mod):
+    """Sharp weights (|logits| up to ~36): B = 3, L = 100 prefill (T = 300, x6 tiles with a
+    partial last tile), a 100-token chunk at 107 (the pruned last block's K / V-only QKV on x6),
+    a decode step; then a batched greedy generation whose prompt prefill runs on x6 (B = 4,
+    L = 80: T = 320), ids exact against the oracle."""
+    args = synth.stories15m(4)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 5, "sharp")
+    m = llama3.Llama(path, args)
+    m.context.set_gemm_x6(True)
+    ref = orc.OracleModel(w, args)
+    rng = np.random.default_rng(19)
+    a = rng.integers(0, args.vocab_size, (3, 100))
+    _close(m(a, 0), ref(a, 0))
+    c = rng.integers(0, args.vocab_size, (3, 100))
+    _close(m(c, 107), ref(c, 107))
+    d = rng.integers(0, args.vocab_size, (3, 1))
+    _close(m(d, 207), ref(d, 207))
+    prompt = rng.integers(0, args.vocab_size, (4, 80))
+    np.testing.assert_array_equal(m.generate_all(prompt, 120), orc.greedy_ids(ref, prompt, 120))
+
+
+@pytest.mark.timeout(600)
+def test_c5_slice_x6_against_golden(c5_weights):
+    """The c5_slice golden (2-layer Llama-3-8B shape, B = 1, L = 256: every layer GEMM of the
+    prefill on x6 — 256 rows against weights past the skinny kernel's range) with the decode
+    steps after it on the fp32 GEMV: logits 1e-4, ids exact."""
+    g = load_golden("c5_slice")
+    m = llama3.Llama(c5_weights[1], synth.llama3_shape(n_layers=2, max_batch_size=1),
+                     keep_host_weights=False)
+    m.context.set_gemm_x6(True)
+    for tag in ("prefill", "dec1", "dec2"):
+        out = m(g[f"{tag}_ids"], int(g[f"{tag}_start"]))
+        want = g[f"{tag}_logits"]
+        assert _close(out, want) <= 1e-4
+        assert int(out[0, -1].argmax()) == int(want[0, -1].argmax())

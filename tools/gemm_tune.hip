@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../llama3.np_amd/csrc/gemm_kernel.h"
+#include "../llama3.np_amd/csrc/gemm_x6.h"
 
 using namespace l3;
 
@@ -75,6 +76,7 @@ static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
 // come from the MALL / HBM as in the batched decode loop (each XCD's 4 MB L2 evicted); per-launch
 // time = (flush + launch) - flush alone, both timed over the same iterations
 static bool g_cold = false;
+static int g_planes_gen = 0;  // x6 planes cache epoch, bumped by every run_shape: a freed buffer's address comes back
 static bool g_qkv_fast = false;  // stamp_report: EPI_QKV with the division-free epilogue
 __global__ void flush_kernel(const f32x4* buf, int64_t n, float* sink) {
     f32x4 a = {0.f, 0.f, 0.f, 0.f};
@@ -96,6 +98,7 @@ static void flush(hipStream_t s) {
 static void run_shape(const char* label, int epi, int M, int K, int N, bool norm,
                       std::vector<Variant> vars, int rounds, int iters) {
     const int outN = epi == EPI_SWIGLU ? N / 2 : (epi == EPI_QKV ? 288 : N);
+    ++g_planes_gen;
     std::vector<float> hA((size_t)M * K), hW((size_t)N * K), hw(K);
     fill(hA, -1.f, 1.f, 1);
     fill(hW, -0.05f, 0.05f, 2);
@@ -386,7 +389,103 @@ static void skinny_stamps(int M, int reps) {
                med(loop[k]) / 100, med(red[k]) / 100, med(epi[k]) / 100, med(ack[k]) / 100);
 }
 
+// x6 (research, gemm_x6.h): the weight (and, for A3, the activation) split into bf16 planes once
+// per buffer on first use, outside the timed launches
+static unsigned short* planes_of(const float* src, int rows, int K, hipStream_t s) {
+    struct Ent { const float* p; int gen; unsigned short* d; };
+    static std::vector<Ent> cache;
+    for (auto& c : cache)
+        if (c.p == src && c.gen == g_planes_gen) return c.d;
+    unsigned short* d;
+    CK(hipMalloc(&d, (size_t)rows * 3 * K * 2));
+    const int64_t n = (int64_t)rows * K;
+    hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, d, (int64_t)rows, K);
+    CK(hipStreamSynchronize(s));
+    cache.push_back({src, g_planes_gen, d});
+    return d;
+}
+#define X6VAR(WM, WN, TM, TN, EPI, WPE)                                                                \
+    Variant{"x6<" #WM "," #WN "," #TM "," #TN ",wpe" #WPE ">", [](const GemmArgs& a0, hipStream_t s) {       \
+                constexpr int BM = WM * TM * 16, BN = WN * TN * 16;                                    \
+                GemmArgs a = a0;                                                                       \
+                a.W3 = planes_of(a.W, a.N, a.K, s);                                                    \
+                const int64_t tiles = (int64_t)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);          \
+                hipLaunchKernelGGL((gemm_x6_kernel<WM, WN, TM, TN, EPI, WPE>), dim3((unsigned)tiles),  \
+                                   dim3(64 * WM * WN), 0, s, a);                                       \
+            }}
+
+// x6acc: C = A W^T (plain store, no norm) from the fp32 MFMA kernel and from the six-product
+// bf16 kernel, each against an fp64 host product on every row: max and rms absolute error
+static void x6_accuracy(int M, int K, int N) {
+    std::vector<float> hA((size_t)M * K), hW((size_t)N * K);
+    fill(hA, -1.f, 1.f, 11);
+    fill(hW, -0.05f, 0.05f, 12);
+    float *A, *W, *C;
+    CK(hipMalloc(&A, hA.size() * 4)); CK(hipMalloc(&W, hW.size() * 4)); CK(hipMalloc(&C, (size_t)M * N * 4));
+    CK(hipMemcpy(A, hA.data(), hA.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(W, hW.data(), hW.size() * 4, hipMemcpyHostToDevice));
+    ++g_planes_gen;
+    GemmArgs g{};
+    g.A = A; g.lda = K; g.W = W; g.C = C; g.ldc = N; g.M = M; g.N = N; g.K = K; g.norm = false;
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    std::vector<double> ref((size_t)M * N);
+    for (int m = 0; m < M; ++m)
+        for (int n = 0; n < N; ++n) {
+            double a = 0;
+            for (int k = 0; k < K; ++k) a += (double)hA[(size_t)m * K + k] * hW[(size_t)n * K + k];
+            ref[(size_t)m * N + n] = a;
+        }
+    std::vector<Variant> vars = {GVAR(2, 2, 4, 4, EPI_STORE, 3, 32), X6VAR(4, 1, 2, 8, EPI_STORE, 2)};
+    std::vector<float> got((size_t)M * N);
+    printf("\n== accuracy against fp64  M=%d K=%d N=%d (A in [-1,1], W in [-0.05,0.05])\n", M, K, N);
+    for (auto& v : vars) {
+        CK(hipMemsetAsync(C, 0, got.size() * 4, s));
+        v.run(g, s);
+        CK(hipStreamSynchronize(s));
+        CK(hipMemcpy(got.data(), C, got.size() * 4, hipMemcpyDeviceToHost));
+        double mx = 0, se = 0, mr = 0;
+        for (size_t i = 0; i < got.size(); ++i) {
+            const double e = std::fabs((double)got[i] - ref[i]);
+            mx = std::max(mx, e);
+            se += e * e;
+            mr = std::max(mr, std::fabs(ref[i]));
+        }
+        printf("   %-40s max|err| %.3e  rms err %.3e  (max|ref| %.3f)\n", v.name.c_str(), mx,
+               std::sqrt(se / got.size()), mr);
+    }
+    CK(hipFree(A)); CK(hipFree(W)); CK(hipFree(C));
+    CK(hipStreamDestroy(s));
+}
+
 int main(int argc, char** argv) {
+    if (argc > 3 && std::string(argv[3]) == "x6acc") {  // error against fp64, both paths
+        x6_accuracy(4096, 288, 1536);
+        x6_accuracy(4096, 768, 288);
+        x6_accuracy(1024, 4096, 4096);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "x6") {  // research: fp32 from six bf16 MFMA products
+        const int rounds = atoi(argv[1]), iters = atoi(argv[2]);
+        run_shape("gate|up (SwiGLU)", EPI_SWIGLU, 65536, 288, 1536, true,
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), X6VAR(4, 1, 2, 8, EPI_SWIGLU, 2),
+                   X6VAR(4, 1, 2, 6, EPI_SWIGLU, 2), X6VAR(4, 2, 2, 4, EPI_SWIGLU, 2),
+                   X6VAR(4, 1, 1, 8, EPI_SWIGLU, 2)},
+                  rounds, iters);
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, 65536, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), X6VAR(4, 1, 2, 6, EPI_QKV, 2),
+                   X6VAR(4, 1, 2, 9, EPI_QKV, 2), X6VAR(4, 1, 1, 9, EPI_QKV, 2)},
+                  rounds, iters);
+        run_shape("down (+resid)", EPI_RESID, 65536, 768, 288, false,
+                  {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), X6VAR(4, 1, 2, 6, EPI_RESID, 2),
+                   X6VAR(4, 1, 2, 9, EPI_RESID, 2), X6VAR(4, 2, 2, 3, EPI_RESID, 2)},
+                  rounds, iters);
+        run_shape("O-proj (+resid)", EPI_RESID, 65536, 288, 288, false,
+                  {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), X6VAR(4, 1, 2, 6, EPI_RESID, 2),
+                   X6VAR(4, 1, 2, 9, EPI_RESID, 2), X6VAR(4, 1, 1, 9, EPI_RESID, 2)},
+                  rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "skinnynw") {  // the K split over 4 / 8 / 16 waves
         for (int r = 0; r < 2; ++r)
             for (int nw : {4, 8, 16}) {
