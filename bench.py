@@ -486,6 +486,40 @@ def bench_c5(a):
                "TFLOP/s": round(flops[k] / (st[k][0] / st[k][1] / 1e3) / 1e12, 1)}
            for k in flops if st[k][1]}
     gu = per["gateup"]["TFLOP/s"]
+    x6 = None
+    if not a.no_x6:
+        # beside the line: the opt-in x6 GEMM path (l3_set_gemm_x6) on the same forward, its
+        # logits against the fp32 path's (the pieces need 1.5x the layer weights: 42 GB here)
+        ctx.forward_dev(ids_dev, B, L, 0, logits_dev)  # the fp32 logits of the whole batch again
+        ctx.d2h(out, logits_dev)
+        ctx.set_gemm_x6(True)
+        ctx.forward_dev(ids_dev, B, L, 0, logits_dev)
+        ctx.synchronize()
+        ctx.kernel_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ctx.forward_dev(ids_dev, B, L, 0, logits_dev)
+        ctx.synchronize()
+        el6 = time.perf_counter() - t0
+        st6 = ctx.kernel_stats()
+        ctx.kernel_timing(False)
+        o6 = np.empty((B, VS), np.float32)
+        ctx.d2h(o6, logits_dev)
+        ctx.set_gemm_x6(False)
+        per6 = {k: {"ms": round(st6[k][0] / st6[k][1], 3),
+                    "TFLOP/s (fp32-equivalent)": round(flops[k] / (st6[k][0] / st6[k][1] / 1e3) / 1e12, 1)}
+                for k in flops if st6[k][1]}
+        gu6 = per6["gateup"]["TFLOP/s (fp32-equivalent)"]
+        x6 = {"value": round(T * a.steps / el6, 1), "unit": "tokens/s", "ms_per_step": round(el6 / a.steps * 1e3, 1),
+              "whole_forward_fp32_equivalent_TFLOP/s": round(total * a.steps / el6 / 1e12, 1),
+              "logits_max_abs_diff_vs_fp32_path": float(np.abs(o6 - out).max()),
+              "argmax_rows_equal_vs_fp32_path": f"{int((o6.argmax(1) == out.argmax(1)).sum())}/{B}",
+              "roofline": {"kernel": "x6 gemm gate|up, M=131072 K=4096 N=28672", "bound": "mfma",
+                           "achieved": gu6, "peak": PEAK_X6_TFLOPS,
+                           "unit": "fp32-equivalent TFLOP/s (6 bf16 MFMA per fp32 product)",
+                           "frac": round(gu6 / PEAK_X6_TFLOPS, 4),
+                           "vs_fp32_mfma_peak": round(gu6 / PEAK_FP32_TFLOPS, 4)},
+              "kernels": per6}
     print(json.dumps({
         "metric": "tokens/s Llama-3-shape prefill B=64 L=2048 (roofline report, BASELINE configs[4])",
         "value": round(T * a.steps / el, 1), "unit": "tokens/s", "n_gpus": 1, "steps": a.steps,
@@ -501,6 +535,7 @@ def bench_c5(a):
                      "traffic": traffic_per_launch(T, "pmc_c5_gateup.json")},
         "kernels": per, "weight_upload_s": round(t_up, 1),
         "output_check": {"all_finite": finite, "row0_vs_B1_run_max_abs": row_err, "tol": "1e-5 abs+rel"},
+        "gemm_x6": x6,
         "lib": {"version": l3hip.version(), "source_hash": l3hip.source_hash()}}))
 
 

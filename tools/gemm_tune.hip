@@ -78,6 +78,7 @@ static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
 static bool g_cold = false;
 static int g_planes_gen = 0;  // x6 planes cache epoch, bumped by every run_shape: a freed buffer's address comes back
 static bool g_qkv_fast = false;  // stamp_report: EPI_QKV with the division-free epilogue
+static bool g_qkv_fast_run = false;  // run_shape: EPI_QKV with the division-free epilogue
 __global__ void flush_kernel(const f32x4* buf, int64_t n, float* sink) {
     f32x4 a = {0.f, 0.f, 0.f, 0.f};
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) a += buf[i];
@@ -126,6 +127,7 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
         CK(hipMemcpy(rc, tc.data(), tc.size() * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(rsn, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
         g.q_out = qo; g.cache_k = ck; g.cache_v = cv; g.rope_cos = rc; g.rope_sin = rsn;
+        g.qkv_fast = g_qkv_fast_run;  // x6 mode: the product's division-free epilogue
         g.C = qo;  // the correctness check reads the q section
         g.ldc = 288;
     }
@@ -465,8 +467,9 @@ int main(int argc, char** argv) {
         x6_accuracy(1024, 4096, 4096);
         return 0;
     }
-    if (argc > 3 && std::string(argv[3]) == "x6") {  // research: fp32 from six bf16 MFMA products
+    if (argc > 3 && std::string(argv[3]) == "x6") {  // fp32 from six bf16 MFMA products (gemm_x6.h)
         const int rounds = atoi(argv[1]), iters = atoi(argv[2]);
+        g_qkv_fast_run = true;
         run_shape("gate|up (SwiGLU)", EPI_SWIGLU, 65536, 288, 1536, true,
                   {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), X6VAR(4, 1, 2, 8, EPI_SWIGLU, 2),
                    X6VAR(4, 1, 2, 6, EPI_SWIGLU, 2), X6VAR(4, 2, 2, 4, EPI_SWIGLU, 2),
@@ -474,7 +477,7 @@ int main(int argc, char** argv) {
                   rounds, iters);
         run_shape("QKV (+RoPE, KV append)", EPI_QKV, 65536, 288, 864, true,
                   {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), X6VAR(4, 1, 2, 6, EPI_QKV, 2),
-                   X6VAR(4, 1, 2, 9, EPI_QKV, 2), X6VAR(4, 1, 1, 9, EPI_QKV, 2)},
+                   X6VAR(4, 2, 2, 3, EPI_QKV, 2), X6VAR(2, 1, 2, 6, EPI_QKV, 2), X6VAR(4, 1, 2, 8, EPI_QKV, 2)},
                   rounds, iters);
         run_shape("down (+resid)", EPI_RESID, 65536, 768, 288, false,
                   {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), X6VAR(4, 1, 2, 6, EPI_RESID, 2),
@@ -482,7 +485,7 @@ int main(int argc, char** argv) {
                   rounds, iters);
         run_shape("O-proj (+resid)", EPI_RESID, 65536, 288, 288, false,
                   {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), X6VAR(4, 1, 2, 6, EPI_RESID, 2),
-                   X6VAR(4, 1, 2, 9, EPI_RESID, 2), X6VAR(4, 1, 1, 9, EPI_RESID, 2)},
+                   X6VAR(4, 2, 2, 3, EPI_RESID, 2), X6VAR(2, 1, 2, 6, EPI_RESID, 2), X6VAR(2, 2, 2, 3, EPI_RESID, 2)},
                   rounds, iters);
         return 0;
     }

@@ -23,11 +23,14 @@ for s in "$@"; do
     bench) step bench 600 python bench.py ;;
     benchq) step benchq 300 python bench.py --no-cpu-baseline ;;
     split[1-4]) L3_BATCH_SPLIT=${s#split} step $s 300 python bench.py --no-cpu-baseline ;;
-    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown ;;
-    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1
-         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 ;;
-    pmcc5) step pmc_c5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_c5_fetch -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1
-         step pmc_c5_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_c5_write -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1 ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --no-x6 ;;
+    profx6) L3_GEMM_X6=1 step profx6 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profx6 -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-kernel-breakdown --no-x6 ;;
+    x6tune) step x6tune 600 tools/gemm_tune 5 10 x6 ;;
+    x6acc) step x6acc 300 tools/gemm_tune 1 1 x6acc ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6
+         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6 ;;
+    pmcc5) step pmc_c5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_c5_fetch -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1 --no-x6
+         step pmc_c5_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_c5_write -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1 --no-x6 ;;
     tune) step tune 600 tools/gemm_tune 5 10 ;;
     tunerows) step tunerows 600 tools/gemm_tune 5 10 rows ;;
     tunering) step tunering 600 tools/gemm_tune 5 10 ring ;;
@@ -105,8 +108,8 @@ for s in "$@"; do
     benchq8) GPU_MAX_HW_QUEUES=8 step benchq8 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
     pmcattn) step pmcattnA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcattnA -o run --output-format csv -- tools/attn_tune 1 2 c3
            step pmcattnB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcattnB -o run --output-format csv -- tools/attn_tune 1 2 c3 ;;
-    pmcgemm) step pmcgemmA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcgemmA -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1
-             step pmcgemmB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcgemmB -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 ;;
+    pmcgemm) step pmcgemmA 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS -d gpurun_out/pmcgemmA -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6
+             step pmcgemmB 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmcgemmB -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6 ;;
     attnprof) step attnprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/attnprof -o run --output-format csv -- tools/attn_tune 3 10 ;;
     loadprobe) step loadprobe 600 python tools/load_probe.py ;;
     new4) step new4 1100 python -u -m pytest tests/test_gpu_parity.py -x -v -rfP -k "group or comm_info or gather or c4_full or c5_full_depth_full_size" --timeout 900 --timeout-method thread ;;
