@@ -20,7 +20,7 @@ static hipError_t launch(const GemmArgs& a, hipStream_t s) {
 }
 
 // the opt-in x6 path (gemm_x6.h): six bf16 MFMA products per fp32 product, W3 pieces from
-// l3_finalize; 64 x WN*TN*16 ... tiles chosen with tools/gemm_tune x6
+// l3_finalize; WM*TM*16 x WN*TN*16 tiles (BK 32, 2 blocks per CU by LDS)
 template <int EPI, int WM, int WN, int TM, int TN>
 static hipError_t launch_x6(const GemmArgs& a, hipStream_t s) {
     constexpr int BM = WM * TM * 16, BN = WN * TN * 16;
@@ -298,14 +298,19 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     // sequences; L3_QKV_FAST_EPI=0 keeps the generic epilogue (A/B; both round identically)
     static const bool qkv_fast_env = env_knob("L3_QKV_FAST_EPI", 1) != 0;
     ag.qkv_fast = epi == EPI_QKV && qkv_fast_env && a.HD % 16 == 0 && a.L >= 64;
-    if (a.W3 && !small_m && epi != EPI_STORE) {  // x6 (opt-in): 128-row tiles of four waves
+    // x6 (opt-in): 128-row tiles, four waves (eight for the O-proj); tools/gemm_tune x6 at C3
+    // (profiles/r06_x6_tiles*.txt): gate|up 128 x 128 187.6-189.2 fp32-equivalent TF/s against
+    // 115.0 for the fp32 kernel on the same box, QKV 128 x 96 153.5, down 128 x 96 175.3, O-proj
+    // 128 x 96 of 8 waves 148.7 (4 waves 141.6)
+    if (a.W3 && !small_m && epi != EPI_STORE) {
         switch (epi) {
             case EPI_SWIGLU: return launch_x6<EPI_SWIGLU, 4, 1, 2, 8>(ag, s);   // 128 x 128
             case EPI_QKV:
                 if (a.N % 96 == 0) return launch_x6<EPI_QKV, 4, 1, 2, 6>(ag, s);  // 128 x 96
                 return launch_x6<EPI_QKV, 4, 1, 2, 8>(ag, s);
-            case EPI_RESID:
-                if (a.N % 96 == 0) return launch_x6<EPI_RESID, 4, 1, 2, 6>(ag, s);
+            case EPI_RESID:  // O-proj (short K): 8 waves of 32 x 48; down: 4 waves of 32 x 96
+                if (a.N % 96 == 0)
+                    return a.K <= 512 ? launch_x6<EPI_RESID, 4, 2, 2, 3>(ag, s) : launch_x6<EPI_RESID, 4, 1, 2, 6>(ag, s);
                 return launch_x6<EPI_RESID, 4, 1, 2, 8>(ag, s);
             default: return hipErrorInvalidValue;
         }

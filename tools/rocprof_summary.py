@@ -27,8 +27,10 @@ def flops(name, T):
             return "gate|up (SwiGLU)", 2.0 * T * D * 2 * FD
         if epi == 3:
             return "QKV (+RMSNorm, RoPE, KV append)", 2.0 * T * D * 3 * D
-        if epi == 1:  # dispatch: 64x96 at K = 288 (O-proj), 128x96 at K = 768 (down)
-            return ("O-proj (+residual)", 2.0 * T * D * D) if tm == 2 else ("down (+residual)", 2.0 * T * FD * D)
+        if epi == 1:  # dispatch: 64x96 at K = 288 (O-proj), 128x96 at K = 768 (down); x6 (gemm_x6.h):
+            # 4 x 2 waves of 32x48 (O-proj), 4 x 1 waves of 32x96 (down)
+            oproj = wn == 2 if "gemm_x6_kernel" in name else tm == 2
+            return ("O-proj (+residual)", 2.0 * T * D * D) if oproj else ("down (+residual)", 2.0 * T * FD * D)
         if epi == 0:
             return "lm_head (+final RMSNorm, last row)", 2.0 * (T // L) * D * VS
     if "attn_fwd_kernel" in name:
@@ -44,7 +46,7 @@ def main():
     ap.add_argument("--trace")
     a = ap.parse_args()
     shutil.copy(a.stats, a.prefix + "_kernel_stats.csv")
-    lines = ["| kernel | role | grid | calls | mean µs | algorithmic TFLOP/s | % of 157.3 |",
+    lines = ["| kernel | role | grid | calls | mean µs | algorithmic TFLOP/s | % of peak (fp32 157.3; x6 419.4 fp32-equivalent) |",
              "|---|---|---|---|---|---|---|"]
     rows = []  # (name, grid, calls, mean ns, total ns)
     if a.trace:
@@ -69,7 +71,8 @@ def main():
         role, fl = flops(name, t)
         us = ns / 1e3
         tf = f"{fl / (us * 1e-6) / 1e12:.1f}" if fl else "-"
-        pc = f"{fl / (us * 1e-6) / 1e12 / 157.3 * 100:.1f}" if fl else "-"
+        peak = 2516.6 / 6 if "gemm_x6_kernel" in name else 157.3  # x6: six bf16 MFMA per fp32 product
+        pc = f"{fl / (us * 1e-6) / 1e12 / peak * 100:.1f}" if fl else "-"
         gs = f"{g} ({t} rows)" if g else "-"
         lines.append(f"| `{name[:60]}` | {role} | {gs} | {calls} | {us:.1f} | {tf} | {pc} |")
     if a.bench:
