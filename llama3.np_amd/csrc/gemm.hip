@@ -309,8 +309,10 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
                 if (a.N % 96 == 0) return launch_x6<EPI_QKV, 4, 1, 2, 6>(ag, s);  // 128 x 96
                 return launch_x6<EPI_QKV, 4, 1, 2, 8>(ag, s);
             case EPI_RESID:  // O-proj (short K): 8 waves of 32 x 48; down: 4 waves of 32 x 96
-                if (a.N % 96 == 0)
-                    return a.K <= 512 ? launch_x6<EPI_RESID, 4, 2, 2, 3>(ag, s) : launch_x6<EPI_RESID, 4, 1, 2, 6>(ag, s);
+                if (a.N % 96 == 0) {
+                    static const bool w8 = env_knob("L3_X6_OPROJ_W8", 1) != 0;  // A/B: 0 = 4 waves
+                    return a.K <= 512 && w8 ? launch_x6<EPI_RESID, 4, 2, 2, 3>(ag, s) : launch_x6<EPI_RESID, 4, 1, 2, 6>(ag, s);
+                }
                 return launch_x6<EPI_RESID, 4, 1, 2, 8>(ag, s);
             default: return hipErrorInvalidValue;
         }

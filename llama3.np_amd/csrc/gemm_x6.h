@@ -95,6 +95,12 @@ __global__ void __launch_bounds__(64 * WM * WN, WPE) gemm_x6_kernel(GemmArgs p) 
     auto a_img = [&](int buf) { return smem + buf * A_BYTES; };
     auto w_img = [&](int buf) { return smem + 2 * A_BYTES + buf * W_BYTES; };
 
+#ifndef L3_X6_VGPR_FORM
+    // an AGPR reference: hipcc then gives the MFMAs the AGPR form (accumulators in a[], D = C in
+    // place) instead of VGPR chains renamed around the VALU work; tools/gemm_tune x6 at C3: QKV
+    // 158.8 vs 153.5, O-proj 154.6 vs 148.7, down 185.2 vs 175.3 fp32-equivalent TF/s
+    asm volatile("" ::: "a0");
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WN, wn = wid % WN;
     const int ntn = (p.N + BN - 1) / BN;

@@ -21,6 +21,6 @@ for sp in $specs; do
   for f in gpurun_out/abbe_v${k}_*.log; do
     echo "$sp $(basename $f) $(python3 -c 'import json,sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
-print("ms", d["ms_per_step"], "median", d["ms_per_step_median"], "host", d["ms_per_step_with_logits_d2h"], "all_rows", d["ms_per_step_all_rows_last_layer"])' $f)"
+print("ms", d["ms_per_step"], "median", d["ms_per_step_median"], "host", d["ms_per_step_with_logits_d2h"], "all_rows", d["ms_per_step_all_rows_last_layer"], "x6", (d.get("gemm_x6") or {}).get("ms_per_step"))' $f)"
   done
 done

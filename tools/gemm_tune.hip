@@ -76,7 +76,8 @@ static void fill(std::vector<float>& v, float lo, float hi, unsigned seed) {
 // come from the MALL / HBM as in the batched decode loop (each XCD's 4 MB L2 evicted); per-launch
 // time = (flush + launch) - flush alone, both timed over the same iterations
 static bool g_cold = false;
-static int g_planes_gen = 0;  // x6 planes cache epoch, bumped by every run_shape: a freed buffer's address comes back
+static int g_planes_gen = 0;
+static int g_repeat_check = 0;  // run_shape: each variant this many more times, outputs compared bit for bit  // x6 planes cache epoch, bumped by every run_shape: a freed buffer's address comes back
 static bool g_qkv_fast = false;  // stamp_report: EPI_QKV with the division-free epilogue
 static bool g_qkv_fast_run = false;  // run_shape: EPI_QKV with the division-free epilogue
 __global__ void flush_kernel(const f32x4* buf, int64_t n, float* sink) {
@@ -169,6 +170,52 @@ static void run_shape(const char* label, int epi, int M, int K, int N, bool norm
             printf("   check %-40s max|diff| %.3e (max|ref| %.3e)%s\n", vars[v].name.c_str(), md, mr,
                    md <= 1e-4 * std::max(1.0, mr) ? "" : "  <-- MISMATCH");
         }
+    }
+    for (size_t v = 0; v < vars.size() && g_repeat_check; ++v) {  // run-to-run determinism
+        std::vector<float> first(got.size()), again(got.size());
+        int bad = 0;
+        for (int r = 0; r <= g_repeat_check; ++r) {
+            CK(hipMemsetAsync(g.C, 0, (size_t)M * outN * 4, s));
+            vars[v].run(g, s);
+            CK(hipStreamSynchronize(s));
+            CK(hipMemcpy(r ? again.data() : first.data(), g.C, got.size() * 4, hipMemcpyDeviceToHost));
+            if (r && again != first) {
+                ++bad;
+                // where: count, max |diff|, the first differing element's row / column and tile
+                size_t n = 0, i0 = SIZE_MAX;
+                double md = 0;
+                for (size_t i = 0; i < again.size(); ++i)
+                    if (again[i] != first[i]) {
+                        ++n;
+                        md = std::max(md, (double)std::fabs(again[i] - first[i]));
+                        if (i0 == SIZE_MAX) i0 = i;
+                    }
+                if (bad <= 5)
+                    printf("      run %d: %zu elements differ, max %.3e, first at row %zu col %zu\n", r, n, md,
+                           i0 / outN, i0 % outN);
+                if (bad == 1 && getenv("X6_DUMP")) {  // where: per 128-row block and per column, samples
+                    std::vector<int> rb(M / 128 + 1), cc(outN);
+                    int shown = 0;
+                    for (size_t i = 0; i < again.size(); ++i)
+                        if (again[i] != first[i]) {
+                            rb[(i / outN) / 128]++;
+                            cc[i % outN]++;
+                            if (shown++ < 24)
+                                printf("        row %zu (seq %zu pos %zu) col %zu: %.6f vs %.6f\n", i / outN, i / outN / 256,
+                                       (i / outN) % 256, i % outN, first[i], again[i]);
+                        }
+                    printf("        row blocks hit:");
+                    int nb = 0;
+                    for (size_t b = 0; b < rb.size(); ++b)
+                        if (rb[b]) { if (nb++ < 40) printf(" %zu:%d", b, rb[b]); }
+                    printf(" (%d blocks)\n        cols hit:", nb);
+                    for (int c = 0; c < outN; ++c)
+                        if (cc[c]) printf(" %d", c);
+                    printf("\n");
+                }
+            }
+        }
+        printf("   repeat %-39s %d of %d runs differ from the first\n", vars[v].name.c_str(), bad, g_repeat_check);
     }
     std::vector<std::vector<double>> tf(vars.size());
     hipEvent_t e0, e1;
@@ -465,6 +512,32 @@ int main(int argc, char** argv) {
         x6_accuracy(4096, 288, 1536);
         x6_accuracy(4096, 768, 288);
         x6_accuracy(1024, 4096, 4096);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "x6detq") {  // QKV only: epilogue forms, tile heights
+        g_repeat_check = argc > 4 ? atoi(argv[4]) : 20;
+        for (int fast = 1; fast >= 0; --fast) {
+            g_qkv_fast_run = fast;
+            printf("\n### qkv_fast %d\n", fast);
+            run_shape("QKV (+RoPE, KV append)", EPI_QKV, 65536, 288, 864, true,
+                      {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), GVAR(2, 2, 2, 3, EPI_QKV, 4, 16), X6VAR(4, 1, 2, 6, EPI_QKV, 2),
+                       X6VAR(2, 2, 4, 3, EPI_QKV, 2)}, 1, 1);
+        }
+        run_shape("QKV shape, plain store", EPI_STORE, 65536, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_STORE, 4, 16), X6VAR(4, 1, 2, 6, EPI_STORE, 2)}, 1, 1);
+        return 0;
+    }
+    if (argc > 3 && std::string(argv[3]) == "x6det") {  // run-to-run determinism of the x6 tiles
+        g_repeat_check = argc > 4 ? atoi(argv[4]) : 20;
+        g_qkv_fast_run = true;
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, 65536, 288, 864, true,
+                  {GVAR(2, 2, 4, 3, EPI_QKV, 4, 16), X6VAR(4, 1, 2, 6, EPI_QKV, 2), X6VAR(4, 1, 2, 8, EPI_QKV, 2)}, 1, 1);
+        run_shape("down (+resid)", EPI_RESID, 65536, 768, 288, false,
+                  {GVAR(2, 2, 4, 3, EPI_RESID, 2, 32), X6VAR(4, 1, 2, 6, EPI_RESID, 2), X6VAR(4, 1, 2, 8, EPI_RESID, 2)}, 1, 1);
+        run_shape("O-proj (+resid)", EPI_RESID, 65536, 288, 288, false,
+                  {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), X6VAR(4, 2, 2, 3, EPI_RESID, 2), X6VAR(4, 1, 2, 6, EPI_RESID, 2)}, 1, 1);
+        run_shape("gate|up (SwiGLU)", EPI_SWIGLU, 65536, 288, 1536, true,
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), X6VAR(4, 1, 2, 8, EPI_SWIGLU, 2), X6VAR(4, 1, 2, 6, EPI_SWIGLU, 2)}, 1, 1);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "x6") {  // fp32 from six bf16 MFMA products (gemm_x6.h)
