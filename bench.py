@@ -958,6 +958,7 @@ def main():
                          "bound": "mfma", "achieved": round(gu6, 2), "peak": PEAK_X6_TFLOPS,
                          "unit": "fp32-equivalent TFLOP/s (6 bf16 MFMA per fp32 product)",
                          "frac": round(gu6 / PEAK_X6_TFLOPS, 4),
+                         "traffic": traffic_per_launch(T, "pmc_x6_gateup.json"),
                          "bf16_mfma_tflops_executed": round(6 * gu6, 1),
                          "vs_fp32_mfma_peak": round(gu6 / PEAK_FP32_TFLOPS, 4),
                          "ffn": {"achieved": round(ffn6, 2), "frac": round(ffn6 / PEAK_X6_TFLOPS, 4)}},

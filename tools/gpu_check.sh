@@ -29,6 +29,8 @@ for s in "$@"; do
     x6acc) step x6acc 300 tools/gemm_tune 1 1 x6acc ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6 ;;
+    pmcx6) L3_GEMM_X6=1 step pmc_x6_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_x6_fetch -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6
+         L3_GEMM_X6=1 step pmc_x6_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_x6_write -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-breakdown --split 1 --no-x6 ;;
     pmcc5) step pmc_c5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_c5_fetch -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1 --no-x6
          step pmc_c5_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_c5_write -o run --output-format csv -- python bench.py --workload c5 --layers 2 --steps 1 --warmup 1 --no-x6 ;;
     tune) step tune 600 tools/gemm_tune 5 10 ;;

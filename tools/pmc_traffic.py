@@ -13,7 +13,8 @@ bytes of a wide coalesced streaming read (TCC_EA0_RDREQ x 64 B for 128-B request
 are doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Both counters are in KiB.
 The guide calibrates the x2 only for 16-B-per-lane coalesced streams, so it is applied only to
 the kernels whose global reads are that (CALIBRATED: the tiled GEMM's A / W tile loads and the
-prefill attention's K / V tile and q loads — whole rows, 16 B per lane, consecutive lanes
+prefill attention's K / V tile and q loads, and the x6 GEMM's activation / weight-piece tiles (the
+same global_load_lds pieces) — whole rows, 16 B per lane, consecutive lanes
 consecutive addresses); every other kernel (decode attention: one key row per thread; GEMV /
 skinny: lane-split rows; fills and copies) is reported "uncalibrated", as the range
 [FETCH + WRITE, 2 x FETCH + WRITE] with no single per-launch figure.
@@ -42,7 +43,7 @@ def load(d, counter):
     return per
 
 
-CALIBRATED = (r"l3::gemm_lds_kernel<", r"l3::attn_fwd_kernel<")
+CALIBRATED = (r"l3::gemm_lds_kernel<", r"l3::gemm_x6_kernel<", r"l3::attn_fwd_kernel<")
 
 
 def calibrated(kernel: str) -> bool:
