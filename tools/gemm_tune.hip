@@ -770,6 +770,16 @@ int main(int argc, char** argv) {
                    GVAR(1, 3, 8, 2, EPI_STORE, 4, 16)}, rounds, iters);
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "lmcold") {  // round 6: batched-decode lm_head, L2 flushed per launch
+        g_cold = true;
+        run_shape("lm_head M=256 (cold)", EPI_STORE, 256, 288, 32000, true,
+                  {GVARN(4, 1, 4, 4, EPI_STORE, 2, 16, 3), GVARN(4, 1, 4, 2, EPI_STORE, 2, 16, 3),
+                   GVARN(4, 1, 4, 2, EPI_STORE, 2, 16, 4), GVARN(4, 1, 4, 1, EPI_STORE, 2, 16, 4),
+                   GVARN(2, 2, 4, 2, EPI_STORE, 2, 16, 4), GVARN(4, 1, 2, 4, EPI_STORE, 2, 16, 4),
+                   GVARN(2, 2, 4, 4, EPI_STORE, 2, 16, 4), GVARN(4, 1, 2, 2, EPI_STORE, 2, 16, 4)},
+                  rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "lmhead") {  // last-position lm_head tiles (C3 part / batched decode)
         // M = 128 (a C3 batch-split part) and 256 (the batch, batched decode B = 256): one block
         // per CU at the product tiles (250 / 500 blocks); smaller tiles put several on each CU
