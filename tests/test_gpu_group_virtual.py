@@ -143,3 +143,31 @@ def test_group_virtual_c4_partition(c4_model, monkeypatch, n):
         np.testing.assert_array_equal(nxt_g[i::n], nxt_s, err_msg=f"member {i} greedy ids")
     print(f"C4 partition n={n}: members bit-identical (per-link host copies and the gather), "
           f"oracle max-abs {err:.2e}")
+
+
+@pytest.mark.timeout(600)
+def test_group_virtual_x6_members_match_single_device(model_path, single, monkeypatch):
+    """The opt-in x6 GEMM path (L3_GEMM_X6=1 at context creation) through the group: at the C3
+    batch each of n = 2 members prefills 128 rows x 256 positions on the x6 kernels, and its rows
+    equal a single-device x6 run of those rows bit for bit (the x6 kernel's per-element
+    arithmetic does not depend on M), greedy ids included."""
+    monkeypatch.setenv("L3_GROUP_VIRTUAL", "1")
+    monkeypatch.setenv("L3_GEMM_X6", "1")
+    args, path = model_path
+    n = 2
+    grp = llama3.Llama(path, args, devices=[0] * n)
+    single_x6 = llama3.Llama(path, args)
+    ids = np.random.default_rng(7).integers(0, args.vocab_size, (256, 256))
+    got = np.array(grp(ids, 0))
+    nxt_g, _ = grp.group.greedy_step(ids[:, :3], 250)
+    # the x6 path ran: the logits are not the fp32 kernels' bits; each path is within the parity
+    # bar of the reference (test_gpu_parity.py: x6 against the oracle on these sharp weights), so
+    # the two differ by at most twice it
+    f32 = single(ids, 0)
+    assert not np.array_equal(got, f32)
+    err = np.abs(got.astype(np.float64) - f32)
+    assert (err <= 2 * (1e-4 + 2e-4 * np.abs(f32))).all(), f"x6 vs fp32 max-abs {err.max():.3e}"
+    for i in range(n):
+        np.testing.assert_array_equal(got[i::n], single_x6(ids[i::n], 0), err_msg=f"x6 member {i}")
+        nxt_s, _ = single_x6.context.greedy_step(ids[i::n, :3], 250)
+        np.testing.assert_array_equal(nxt_g[i::n], nxt_s, err_msg=f"x6 member {i} greedy ids")
