@@ -298,13 +298,15 @@ hipError_t launch_gemm(int epi, const GemmArgs& a, hipStream_t s) {
     // sequences; L3_QKV_FAST_EPI=0 keeps the generic epilogue (A/B; both round identically)
     static const bool qkv_fast_env = env_knob("L3_QKV_FAST_EPI", 1) != 0;
     ag.qkv_fast = epi == EPI_QKV && qkv_fast_env && a.HD % 16 == 0 && a.L >= 64;
-    // x6 (opt-in): 128-row tiles, four waves (eight for the O-proj); tools/gemm_tune x6 at C3
+    // x6 (opt-in): 128-row tiles, four waves (eight for gate|up and the O-proj); tools/gemm_tune x6 at C3
     // (profiles/r06_x6_tiles*.txt, final build r06_x6_tiles_final.txt): gate|up 128 x 128 195.0
     // fp32-equivalent TF/s against 119.7 for the fp32 kernel on the same box, QKV 128 x 128 162.0
-    // (128 x 96 158.1), down 128 x 96 178.7, O-proj 128 x 96 of 8 waves 151.8 (4 waves 145.4)
+    // (128 x 96 158.1), down 128 x 96 178.7, O-proj 128 x 96 of 8 waves 151.8 (4 waves 145.4);
+    // gate|up on 8 waves of 16 x 128 193.9 vs 186.2 for 4 of 32 x 128 (r06_x6_big.txt), C3 x6
+    // step 4.505-4.509 vs 4.552-4.569 ms (r06_x6_gateup8_ab.txt)
     if (a.W3 && !small_m && epi != EPI_STORE) {
         switch (epi) {
-            case EPI_SWIGLU: return launch_x6<EPI_SWIGLU, 4, 1, 2, 8>(ag, s);   // 128 x 128
+            case EPI_SWIGLU: return launch_x6<EPI_SWIGLU, 8, 1, 1, 8>(ag, s);   // 128 x 128, 8 waves
             case EPI_QKV:  // 128 x 128 (C3's 864 columns: 6 3/4 tiles, the last on the generic epilogue)
                 return launch_x6<EPI_QKV, 4, 1, 2, 8>(ag, s);
             case EPI_RESID:  // O-proj (short K): 8 waves of 32 x 48; down: 4 waves of 32 x 96

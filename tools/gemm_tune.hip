@@ -527,6 +527,21 @@ int main(int argc, char** argv) {
                   {GVAR(2, 2, 4, 3, EPI_STORE, 4, 16), X6VAR(4, 1, 2, 6, EPI_STORE, 2)}, 1, 1);
         return 0;
     }
+    if (argc > 3 && std::string(argv[3]) == "x6big") {  // 8-wave x6 blocks (one per CU by LDS)
+        const int rounds = atoi(argv[1]), iters = atoi(argv[2]);
+        g_qkv_fast_run = true;
+        run_shape("gate|up (SwiGLU)", EPI_SWIGLU, 65536, 288, 1536, true,
+                  {X6VAR(4, 1, 2, 8, EPI_SWIGLU, 2), X6VAR(8, 1, 2, 8, EPI_SWIGLU, 1), X6VAR(4, 2, 2, 8, EPI_SWIGLU, 1),
+                   X6VAR(4, 2, 2, 4, EPI_SWIGLU, 2), X6VAR(8, 1, 1, 8, EPI_SWIGLU, 2)},
+                  rounds, iters);
+        run_shape("down (+resid)", EPI_RESID, 65536, 768, 288, false,
+                  {X6VAR(4, 1, 2, 6, EPI_RESID, 2), X6VAR(8, 1, 2, 6, EPI_RESID, 1), X6VAR(4, 2, 2, 6, EPI_RESID, 1)},
+                  rounds, iters);
+        run_shape("QKV (+RoPE, KV append)", EPI_QKV, 65536, 288, 864, true,
+                  {X6VAR(4, 1, 2, 8, EPI_QKV, 2), X6VAR(8, 1, 2, 8, EPI_QKV, 1), X6VAR(8, 1, 2, 6, EPI_QKV, 1)},
+                  rounds, iters);
+        return 0;
+    }
     if (argc > 3 && std::string(argv[3]) == "x6det") {  // run-to-run determinism of the x6 tiles
         g_repeat_check = argc > 4 ? atoi(argv[4]) : 20;
         g_qkv_fast_run = true;
@@ -537,7 +552,7 @@ int main(int argc, char** argv) {
         run_shape("O-proj (+resid)", EPI_RESID, 65536, 288, 288, false,
                   {GVAR(2, 2, 2, 3, EPI_RESID, 3, 32), X6VAR(4, 2, 2, 3, EPI_RESID, 2), X6VAR(4, 1, 2, 6, EPI_RESID, 2)}, 1, 1);
         run_shape("gate|up (SwiGLU)", EPI_SWIGLU, 65536, 288, 1536, true,
-                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), X6VAR(4, 1, 2, 8, EPI_SWIGLU, 2), X6VAR(4, 1, 2, 6, EPI_SWIGLU, 2)}, 1, 1);
+                  {GVAR(2, 2, 4, 4, EPI_SWIGLU, 3, 16), X6VAR(8, 1, 1, 8, EPI_SWIGLU, 2), X6VAR(4, 1, 2, 8, EPI_SWIGLU, 2)}, 1, 1);
         return 0;
     }
     if (argc > 3 && std::string(argv[3]) == "x6") {  // fp32 from six bf16 MFMA products (gemm_x6.h)
