@@ -613,6 +613,7 @@ static void free_x6(l3_ctx* c) {
 
 static int make_x6(l3_ctx* c) {
     const int64_t D = c->d.dim, FD = c->d.hidden_dim;
+    hipError_t e = hipSuccess;
     for (auto& L : c->layers) {
         if (L.wqkv3) continue;
         if (hipMalloc(&L.wqkv3, c->qkvn * D * 6) || hipMalloc(&L.wo3, D * c->qdim * 6) ||
@@ -620,25 +621,39 @@ static int make_x6(l3_ctx* c) {
             free_x6(c);
             return fail("l3_set_gemm_x6: out of device memory (1.5x the layer weights)");
         }
-        HIP_TRY(launch_split_planes(L.wqkv, L.wqkv3, c->qkvn, (int)D, c->stream));
-        HIP_TRY(launch_split_planes(L.wo, L.wo3, D, c->qdim, c->stream));
-        HIP_TRY(launch_split_planes(L.wgu, L.wgu3, 2 * FD, (int)D, c->stream));
-        HIP_TRY(launch_split_planes(L.wd, L.wd3, D, (int)FD, c->stream));
+        if (e == hipSuccess) e = launch_split_planes(L.wqkv, L.wqkv3, c->qkvn, (int)D, c->stream);
+        if (e == hipSuccess) e = launch_split_planes(L.wo, L.wo3, D, c->qdim, c->stream);
+        if (e == hipSuccess) e = launch_split_planes(L.wgu, L.wgu3, 2 * FD, (int)D, c->stream);
+        if (e == hipSuccess) e = launch_split_planes(L.wd, L.wd3, D, (int)FD, c->stream);
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {  // no half-made pieces: the GEMMs run on them as soon as they exist
+        (void)hipStreamSynchronize(c->stream);
+        free_x6(c);
+        return fail("l3_set_gemm_x6: making the weight pieces failed: %s", hipGetErrorString(e));
+    }
     return 0;
 }
 
+// Switching the path: queued run-ahead decode steps are settled first and the captured decode
+// graphs dropped (their launches hold the weight pointers, the pieces included), so no replay
+// can read freed pieces or run the other arithmetic; a failure leaves the fp32 path on
 extern "C" int l3_set_gemm_x6(l3_ctx* c, int32_t on) {
     CHECK_CTX(c);
-    if (set_dev(c)) return 1;
-    c->gemm_x6 = on != 0;
-    if (!c->gemm_x6) {
-        HIP_TRY(hipStreamSynchronize(c->stream));
+    if (set_dev(c) || spec_resolve(c)) return 1;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    drop_decode_graph(c);
+    if (!on) {
+        c->gemm_x6 = false;
         free_x6(c);
         return 0;
     }
-    return c->finalized ? make_x6(c) : 0;  // else l3_finalize makes them
+    c->gemm_x6 = true;
+    if (c->finalized && make_x6(c)) {  // else l3_finalize makes them
+        c->gemm_x6 = false;
+        return 1;
+    }
+    return 0;
 }
 
 extern "C" int l3_finalize(l3_ctx* c) {
@@ -667,7 +682,10 @@ extern "C" int l3_finalize(l3_ctx* c) {
         c->folded_lm = true;
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->gemm_x6 && make_x6(c)) return 1;
+    if (c->gemm_x6 && make_x6(c)) {  // asked for (L3_GEMM_X6) and not made: fail, pieces freed
+        c->gemm_x6 = false;
+        return 1;
+    }
     c->finalized = true;
     return 0;
 }

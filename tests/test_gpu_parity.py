@@ -1357,3 +1357,28 @@ def test_c5_slice_x6_against_golden(c5_weights):
         want = g[f"{tag}_logits"]
         assert _close(out, want) <= 1e-4
         assert int(out[0, -1].argmax()) == int(want[0, -1].argmax())
+
+
+def test_x6_toggle_between_captured_decodes(tmpdir_mod):
+    """Switching the x6 path drops the captured decode graphs (their launches hold the GEMMs'
+    weight pointers, the x6 pieces included) and settles any run-ahead first: a batched greedy
+    generation, the same with x6 on (its 40 x 12-token prefill on the x6 kernels), then off again
+    — ids equal to the oracle's every time, and a lazy generator left mid-way before a switch is
+    undone as for any other off-schedule call."""
+    args = synth.stories15m(40)
+    w, path = _model(tmpdir_mod, args, synth.STORIES15M_HIDDEN, 3, "default")
+    m = llama3.Llama(path, args)
+    ref = orc.OracleModel(w, args)
+    prompt = np.random.default_rng(5).integers(0, args.vocab_size, (40, 12))
+    want = orc.greedy_ids(ref, prompt, 40)
+    np.testing.assert_array_equal(m.generate_all(prompt, 40), want)
+    m.context.set_gemm_x6(True)
+    np.testing.assert_array_equal(m.generate_all(prompt, 40), want)
+    one = prompt[:1]
+    gen = m.generate(one, 30)
+    next(gen), next(gen)  # a lazy generator with run-ahead steps queued, then dropped
+    del gen
+    m.context.set_gemm_x6(False)
+    np.testing.assert_array_equal(m.generate_all(prompt, 40), want)
+    np.testing.assert_array_equal(np.concatenate(list(m.generate(one, 30)), axis=1),
+                                  orc.greedy_ids(orc.OracleModel(w, synth.stories15m(1)), one, 30))
